@@ -1,0 +1,985 @@
+// ============================================================================================
+//  ORACLE — TEST INFRASTRUCTURE ONLY.  Never linked into the product library.
+//
+//  A C++17 CPU restatement of josephg/text-crdt-rust's list CRDT hot path, following the
+//  reference's own B-tree (range_tree), its order index, RLE tables and ListCRDT logic
+//  function by function, so that the *entry layout* (not just the item-level result) matches
+//  the reference for a given (leaf_cap, node_cap).  Release build = 32/16, debug = 4/8
+//  (src/range_tree/mod.rs:29-39).
+//
+//  The reference cannot be compiled here (pure Rust, no cargo/rustc, no crates),
+//  so parity is pinned by the reference's own fixtures: the final document lengths of the three
+//  benchmark traces (benches/yjs.rs:46 assertion, endContent), and the known-answer unit tests
+//  ported in tests/test_oracle.py (double_delete.rs:114-139, simple_rle.rs:119-155,
+//  txn.rs:68-92, doc.rs:571-587, doc.rs:620-676, cursor.rs:318-339).
+//
+//  Used by: tests/ (checker), __graft_entry__.smoke() (checker), bench.py cpu_baseline leg.
+// ============================================================================================
+#pragma once
+#include <algorithm>
+#include <cassert>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace orc {
+using u8 = uint8_t;
+using u16 = uint16_t;
+using u32 = uint32_t;
+using i32 = int32_t;
+using u64 = uint64_t;
+using i64 = int64_t;
+
+constexpr u32 ROOT_ORDER = 0xFFFFFFFFu;  // src/list/mod.rs:30
+constexpr u16 ROOT_AGENT = 0xFFFFu;      // doc.rs:68 ("ROOT" -> AgentId::MAX)
+
+// Status codes, identical to include/crdt_gpu.h
+enum Status : int {
+  OK = 0,
+  ERR_POS_OOB = -1,         // local op outside the document (root.rs:71,79; mutations.rs:573 panic)
+  ERR_SEQ = -2,             // remote txn seq != next seq (doc.rs:247 assert)
+  ERR_UNKNOWN_AGENT = -3,   // get_agent_id(..).unwrap() / client_data[agent] OOB (doc.rs:92,237)
+  ERR_UNKNOWN_ID = -4,      // seq_to_order unwrap / leaf.find expect (doc.rs:27, root.rs:288)
+  ERR_NONTERMINATING = -5,  // the reference's integrate/delete loop would never exit (see integrate)
+  ERR_CAPACITY = -6,        // (GPU only) a per-document capacity was exceeded
+  ERR_EMPTY_TXN = -7,       // zero-length txn: reference computes first_order+0-1 (doc.rs:351)
+  ERR_FRONTIER = -8,        // advance_branch_by assert (doc.rs:43)
+  ERR_BAD_INPUT = -9,       // zero-length remote Ins/Del, malformed record
+};
+
+// ---------------------------------------------------------------------------------------------
+// YjsSpan  (src/list/span.rs:5-119)
+// ---------------------------------------------------------------------------------------------
+struct Span {
+  u32 order = 0, ol = 0, orr = 0;
+  i32 len = 0;  // negative = deleted
+};
+inline u32 slen(const Span& s) { return (u32)(s.len < 0 ? -s.len : s.len); }          // :104
+inline u32 clen(const Span& s) { return s.len > 0 ? (u32)s.len : 0u; }                 // :106
+inline i32 sgn(i32 x) { return (x > 0) - (x < 0); }
+inline u32 origin_left_at_offset(const Span& s, u32 at) { return at == 0 ? s.ol : s.order + at - 1; }  // :23
+inline Span truncate(Span& s, u32 at) {                                                 // :33-45
+  i32 at_s = (i32)at * sgn(s.len);
+  Span o{s.order + at, s.order + at - 1, s.orr, s.len - at_s};
+  s.len = at_s;
+  return o;
+}
+inline Span truncate_keeping_right(Span& s, u32 at) {                                   // :68-85
+  i32 at_s = (i32)at * sgn(s.len);
+  Span o{s.order, s.ol, s.orr, at_s};
+  s.order += at;
+  s.ol = s.order - 1;
+  s.len -= at_s;
+  return o;
+}
+inline bool can_append(const Span& a, const Span& b) {                                 // :47-53
+  return ((a.len > 0) == (b.len > 0)) && b.order == a.order + slen(a) && b.ol == b.order - 1 &&
+         b.orr == a.orr;
+}
+inline void append(Span& a, const Span& b) { a.len += b.len; }
+inline void prepend(Span& a, const Span& b) { a.order = b.order; a.len += b.len; }
+inline bool operator==(const Span& a, const Span& b) {
+  return a.order == b.order && a.ol == b.ol && a.orr == b.orr && a.len == b.len;
+}
+
+// ---------------------------------------------------------------------------------------------
+// RangeTree<YjsSpan, ContentIndex>  (src/range_tree/*)
+// ---------------------------------------------------------------------------------------------
+struct Internal;
+struct NodeBase {
+  bool leaf;
+  Internal* parent;  // nullptr = parent is the tree root
+};
+struct Leaf : NodeBase {
+  Span data[33];  // [0, cap) used; data[cap] stays default (guards data[num_entries] reads)
+  u32 n = 0;
+  Leaf() { leaf = true; parent = nullptr; }
+};
+struct Internal : NodeBase {
+  u32 cnt[16];
+  NodeBase* ch[16];
+  Internal() {
+    leaf = false;
+    parent = nullptr;
+    for (int i = 0; i < 16; i++) { cnt[i] = 0; ch[i] = nullptr; }
+  }
+};
+struct Cursor {
+  Leaf* node;
+  u32 idx;
+  u32 off;
+};
+
+struct OrderIndex;  // order -> leaf (the reference's SplitList, split_list/mod.rs)
+
+struct Tree {
+  u32 L, NC;  // NUM_LEAF_ENTRIES, NUM_NODE_CHILDREN
+  u32 count = 0;
+  NodeBase* root = nullptr;
+  std::vector<std::unique_ptr<Leaf>> leaves;
+  std::vector<std::unique_ptr<Internal>> internals;
+  OrderIndex* index = nullptr;  // notify target (ListCRDT::notify, doc.rs:143-153)
+  bool track_index = true;
+
+  Tree(u32 L_, u32 NC_) : L(L_), NC(NC_) {
+    leaves.emplace_back(new Leaf());
+    root = leaves.back().get();
+  }
+  Leaf* new_leaf() { leaves.emplace_back(new Leaf()); return leaves.back().get(); }
+  Internal* new_internal() { internals.emplace_back(new Internal()); return internals.back().get(); }
+
+  void notify(const Span& e, Leaf* leaf);
+
+  static u32 count_children(const Internal* n, u32 NC) {   // internal.rs:69-73
+    for (u32 i = 0; i < NC; i++) if (!n->ch[i]) return i;
+    return NC;
+  }
+  static int find_child(const Internal* n, const NodeBase* c) {  // internal.rs:86-91
+    for (int i = 0; i < 16; i++) if (n->ch[i] == c) return i;
+    return -1;
+  }
+
+  // leaf.rs:97-125
+  void update_parent_count(Leaf* leaf, i64 amt) {
+    if (amt == 0) return;
+    NodeBase* child = leaf;
+    Internal* p = leaf->parent;
+    while (p) {
+      int idx = find_child(p, child);
+      p->cnt[idx] = (u32)((i64)p->cnt[idx] + amt);
+      child = p;
+      p = p->parent;
+    }
+    count = (u32)((i64)count + amt);
+  }
+  void flush(Leaf* leaf, i64& marker) { i64 a = marker; marker = 0; update_parent_count(leaf, a); }
+
+  // cursor.rs:26-103
+  bool traverse(Cursor& c, bool fwd) {
+    NodeBase* node_ptr = c.node;
+    Internal* parent = c.node->parent;
+    while (true) {
+      if (!parent) return false;
+      int idx = find_child(parent, node_ptr);
+      int next_idx = -1;
+      if (fwd) {
+        if (idx + 1 < (int)NC && parent->ch[idx + 1]) next_idx = idx + 1;
+      } else if (idx > 0) {
+        next_idx = idx - 1;
+      }
+      if (next_idx >= 0) { node_ptr = parent->ch[next_idx]; break; }
+      node_ptr = parent;
+      parent = parent->parent;
+    }
+    while (!node_ptr->leaf) {
+      Internal* in = (Internal*)node_ptr;
+      u32 ni = fwd ? 0 : count_children(in, NC) - 1;
+      node_ptr = in->ch[ni];
+    }
+    Leaf* lf = (Leaf*)node_ptr;
+    c.node = lf;
+    if (fwd) { c.idx = 0; c.off = 0; }
+    else { c.idx = lf->n - 1; c.off = slen(lf->data[c.idx]); }
+    return true;
+  }
+  // cursor.rs:127-145
+  bool next_entry(Cursor& c, i64* marker = nullptr) {
+    if (c.idx + 1 < c.node->n) { c.idx++; c.off = 0; return true; }
+    if (marker) flush(c.node, *marker);
+    return traverse(c, true);
+  }
+  // cursor.rs:210-231
+  bool roll_to_next_entry(Cursor& c) {
+    u32 seq_len = slen(c.node->data[c.idx]);
+    if (c.off == seq_len) {
+      c.off = 0;
+      c.idx++;
+      if (c.idx >= c.node->n) return next_entry(c);
+    }
+    return true;
+  }
+  // cursor.rs:233-239
+  bool get_item(const Cursor& c0, u32& out) {
+    Cursor c = c0;
+    if (roll_to_next_entry(c)) { out = c.node->data[c.idx].order + c.off; return true; }
+    return false;
+  }
+  // cursor.rs:242-248
+  bool next(Cursor& c) {
+    if (!roll_to_next_entry(c)) return false;
+    c.off++;
+    return true;
+  }
+  // cursor.rs:274-304
+  int cmp(const Cursor& a, const Cursor& b) const {
+    if (a.node == b.node) {
+      if (a.idx == b.idx) return (a.off > b.off) - (a.off < b.off);
+      return (a.idx > b.idx) - (a.idx < b.idx);
+    }
+    NodeBase* n1 = a.node;
+    NodeBase* n2 = b.node;
+    while (true) {
+      Internal* p1 = n1->parent;
+      Internal* p2 = n2->parent;
+      if (p1 == p2) {
+        int i1 = find_child(p1, n1), i2 = find_child(p1, n2);
+        return (i1 > i2) - (i1 < i2);
+      }
+      n1 = p1;
+      n2 = p2;
+    }
+  }
+  // root.rs:133-150
+  Cursor cursor_at_start() const {
+    NodeBase* n = root;
+    while (!n->leaf) n = ((Internal*)n)->ch[0];
+    return Cursor{(Leaf*)n, 0, 0};
+  }
+  // root.rs:90-123 (n==0 -> the reference underflows usize; reported as an error by callers)
+  bool cursor_at_end(Cursor& c) const {
+    NodeBase* n = root;
+    while (!n->leaf) { Internal* in = (Internal*)n; n = in->ch[count_children(in, NC) - 1]; }
+    Leaf* lf = (Leaf*)n;
+    if (lf->n == 0) return false;
+    c = Cursor{lf, lf->n - 1, slen(lf->data[lf->n - 1])};
+    return true;
+  }
+  // root.rs:54-88 + 401-411 (ContentIndex, stick_end=false); internal.rs:27-46; leaf.rs:61-84
+  bool cursor_at_content_pos(u32 pos, Cursor& out) const {
+    NodeBase* n = root;
+    u32 rem = pos;
+    while (!n->leaf) {
+      Internal* in = (Internal*)n;
+      NodeBase* next = nullptr;
+      for (u32 i = 0; i < NC; i++) {
+        if (!in->ch[i]) return false;  // "Internal consistency violation"
+        if (rem < in->cnt[i]) { next = in->ch[i]; break; }
+        rem -= in->cnt[i];
+      }
+      if (!next) return false;
+      n = next;
+    }
+    Leaf* lf = (Leaf*)n;
+    for (u32 i = 0; i < lf->n; i++) {
+      const Span& e = lf->data[i];
+      if (e.order == ROOT_ORDER || e.len == 0) break;  // !is_valid()
+      u32 el = clen(e);
+      if (rem < el) { out = Cursor{lf, i, rem}; return true; }
+      rem -= el;
+    }
+    if (rem == 0) { out = Cursor{lf, lf->n, 0}; return true; }
+    return false;
+  }
+  // leaf.rs:41-57 (cursor_before_item, root.rs:286-290)
+  static bool leaf_find(Leaf* lf, u32 order, Cursor& out) {
+    for (u32 i = 0; i < lf->n; i++) {
+      const Span& e = lf->data[i];
+      if (order >= e.order && order < e.order + slen(e)) { out = Cursor{lf, i, order - e.order}; return true; }
+    }
+    return false;
+  }
+
+  // mutations.rs:17-179
+  void insert_internal(const Span* items, u32 nitems, Cursor& c, i64& marker) {
+    if (nitems == 0) return;
+    Leaf* node = c.node;
+    if (c.off == 0 && c.idx > 0) {
+      c.idx -= 1;
+      c.off = slen(node->data[c.idx]);
+    }
+    u32 seq_len = slen(node->data[c.idx]);
+    bool has_rem = false;
+    Span rem{};
+    if (!(c.off == seq_len || c.off == 0)) {
+      rem = truncate(node->data[c.idx], c.off);
+      marker -= clen(rem);
+      has_rem = true;
+    }
+    if (c.off != 0) {
+      u32 it = 0;
+      Span& cur = node->data[c.idx];
+      while (it < nitems) {
+        const Span& nx = items[it];
+        if (can_append(cur, nx)) {
+          marker += clen(nx);
+          notify(nx, c.node);
+          append(cur, nx);
+          c.off = slen(cur);
+          it++;
+        } else break;
+      }
+      if (it == nitems && !has_rem) return;
+      items += it;
+      nitems -= it;
+      c.off = 0;
+      c.idx += 1;
+      if (!has_rem && c.idx < node->n) {
+        int end_idx = (int)nitems - 1;
+        Span& cur2 = node->data[c.idx];
+        while (true) {
+          const Span& nx = items[end_idx];
+          if (can_append(nx, cur2)) {
+            marker += clen(nx);
+            notify(nx, c.node);
+            prepend(cur2, nx);
+          } else break;
+          if (end_idx == 0) return;
+          end_idx--;
+        }
+        nitems = (u32)end_idx + 1;
+      }
+    }
+    u32 space = nitems + (has_rem ? 1 : 0);
+    u32 filled = node->n;
+    if (space > L / 2) std::abort();  // assert (mutations.rs:121)
+    bool rem_moved = false;
+    if (filled + space > L) {
+      flush(node, marker);
+      if (c.idx < L / 2) {
+        split_at(node, c.idx, 0);
+        node->n += space;
+      } else {
+        Leaf* nn = split_at(node, c.idx, space);
+        c.node = nn;
+        c.idx = 0;
+        node = nn;
+        rem_moved = true;
+      }
+    } else {
+      if (filled > c.idx) std::memmove(&node->data[c.idx + space], &node->data[c.idx], sizeof(Span) * (filled - c.idx));
+      node->n += space;
+    }
+    for (u32 i = 0; i < nitems; i++) { marker += clen(items[i]); notify(items[i], c.node); }
+    for (u32 i = 0; i < nitems; i++) node->data[c.idx + i] = items[i];
+    c.idx += nitems - 1;
+    c.off = slen(items[nitems - 1]);
+    if (has_rem) {
+      marker += clen(rem);
+      if (rem_moved) notify(rem, c.node);
+      node->data[c.idx + 1] = rem;
+    }
+  }
+  // mutations.rs:185-200
+  void replace_entry(Cursor& c, const Span* items, u32 nitems, i64& marker) {
+    Span& e = c.node->data[c.idx];
+    marker -= clen(e);
+    e = items[0];
+    marker += clen(e);
+    c.off = slen(e);
+    insert_internal(items + 1, nitems - 1, c, marker);
+  }
+  // mutations.rs:202-224
+  void insert(Cursor c, const Span& e) {
+    i64 marker = 0;
+    insert_internal(&e, 1, c, marker);
+    flush(c.node, marker);
+  }
+  // mutations.rs:227-277.  kind: 0 = local (extend_delete + deactivate), 1 = remote (deactivate)
+  u32 mutate_entry(Cursor& c, u32 replace_max, i64& marker, std::vector<Span>* del_result) {
+    Leaf* node = c.node;
+    Span entry = node->data[c.idx];
+    u32 entry_len = slen(entry);
+    if (!(c.off < entry_len)) std::abort();
+    bool has_a = false, has_c = false;
+    Span a{}, cc{};
+    if (c.off > 0) {
+      entry_len -= c.off;
+      a = truncate_keeping_right(entry, c.off);
+      has_a = true;
+    }
+    u32 replaced;
+    if (replace_max < entry_len) { cc = truncate(entry, replace_max); has_c = true; replaced = replace_max; }
+    else replaced = entry_len;
+    if (del_result) {  // extend_delete (root.rs:9-17) on the still-active entry
+      if (!del_result->empty() && can_append(del_result->back(), entry)) append(del_result->back(), entry);
+      else del_result->push_back(entry);
+    }
+    entry.len = -entry.len;  // mark_deactivated (span.rs:115-118)
+    if (has_a && has_c) { Span it[3] = {a, entry, cc}; replace_entry(c, it, 3, marker); }
+    else if (has_a) { Span it[2] = {a, entry}; replace_entry(c, it, 2, marker); }
+    else if (has_c) { Span it[2] = {entry, cc}; replace_entry(c, it, 2, marker); }
+    else {
+      marker -= clen(node->data[c.idx]);
+      node->data[c.idx] = entry;
+      c.off = replaced;
+      marker += clen(entry);
+    }
+    return replaced;
+  }
+  // mutations.rs:520-570.  Returns false if the delete ran past the end (reference panics).
+  bool local_deactivate(Cursor c, u32 deleted_len, std::vector<Span>& result) {
+    i64 marker = 0;
+    u32 remaining = deleted_len;
+    roll_to_next_entry(c);
+    while (remaining > 0) {
+      while (c.node->data[c.idx].len < 0 || c.node->data[c.idx].len == 0) {
+        if (!next_entry(c, &marker)) return false;  // next_entry_or_panic
+      }
+      remaining -= mutate_entry(c, remaining, marker, &result);
+    }
+    flush(c.node, marker);
+    return true;
+  }
+  // mutations.rs:579-615
+  i64 remote_deactivate(Cursor c, u32 max_len) {
+    roll_to_next_entry(c);
+    Span e = c.node->data[c.idx];
+    if (e.len > 0) {
+      i64 marker = 0;
+      u32 amt = mutate_entry(c, max_len, marker, nullptr);
+      flush(c.node, marker);
+      return (i64)amt;
+    }
+    u32 avail = slen(e) - c.off;
+    return -(i64)std::min(max_len, avail);
+  }
+  // mutations.rs:623-669
+  Leaf* split_at(Leaf* self, u32 idx, u32 padding) {
+    Leaf* nn = new_leaf();
+    u32 new_filled = self->n - idx;
+    u32 new_len = new_filled + padding;
+    if (new_filled > 0) std::memcpy(&nn->data[padding], &self->data[idx], sizeof(Span) * new_filled);
+    nn->n = new_len;
+    u32 stolen = 0;
+    for (u32 i = idx; i < self->n; i++) { stolen += clen(self->data[i]); self->data[i] = Span{}; }
+    self->n = idx;
+    for (u32 i = padding; i < new_len; i++) notify(nn->data[i], nn);
+    insert_after(self->parent, nn, self, stolen);
+    return nn;
+  }
+  // mutations.rs:675-808
+  void insert_after(Internal* parent, NodeBase* inserted, NodeBase* after, u32 stolen) {
+    while (true) {
+      if (parent) {
+        u32 count = count_children(parent, NC);
+        if (count < NC) {
+          inserted->parent = parent;
+          int old_idx = find_child(parent, after);
+          parent->cnt[old_idx] -= stolen;
+          splice_in(parent, old_idx + 1, stolen, inserted);
+          return;
+        }
+      }
+      if (!parent) {
+        Internal* nr = new_internal();
+        NodeBase* old_root = root;
+        u32 c = count - stolen;
+        old_root->parent = nr;
+        inserted->parent = nr;
+        nr->cnt[0] = c; nr->ch[0] = old_root;
+        nr->cnt[1] = stolen; nr->ch[1] = inserted;
+        nr->parent = nullptr;
+        root = nr;
+        return;
+      }
+      Internal* left = parent;
+      parent = left->parent;
+      Internal* right = new_internal();
+      right->parent = parent;
+      int old_idx = find_child(left, after);
+      left->cnt[old_idx] -= stolen;
+      u32 new_stolen = 0;
+      u32 H = NC / 2;
+      if ((u32)old_idx < H) {
+        for (u32 i = 0; i < H; i++) {
+          u32 c = left->cnt[i + H];
+          NodeBase* e = left->ch[i + H];
+          left->cnt[i + H] = 0; left->ch[i + H] = nullptr;
+          if (e) { e->parent = right; new_stolen += c; right->cnt[i] = c; right->ch[i] = e; }
+        }
+        inserted->parent = left;
+        splice_in(left, old_idx + 1, stolen, inserted);
+      } else {
+        u32 new_idx = old_idx - H + 1;
+        inserted->parent = right;
+        bool placed = false;
+        new_stolen = stolen;
+        u32 src = H;
+        for (u32 dest = 0; dest <= H; dest++) {
+          if (dest == new_idx) { right->cnt[dest] = stolen; right->ch[dest] = inserted; placed = true; }
+          else {
+            if (src >= NC) break;
+            u32 c = left->cnt[src];
+            NodeBase* e = left->ch[src];
+            left->cnt[src] = 0; left->ch[src] = nullptr;
+            if (e) { e->parent = right; new_stolen += c; right->cnt[dest] = c; right->ch[dest] = e; src++; }
+            else break;
+          }
+        }
+        (void)placed;
+      }
+      after = left;
+      inserted = right;
+      stolen = new_stolen;
+    }
+  }
+  void splice_in(Internal* n, u32 idx, u32 cnt, NodeBase* elem) {  // internal.rs:49-67
+    u32 bc = cnt;
+    NodeBase* be = elem;
+    for (u32 i = idx; i < NC; i++) {
+      std::swap(bc, n->cnt[i]);
+      std::swap(be, n->ch[i]);
+      if (!be) break;
+    }
+  }
+
+  // Walk leaves in document order.
+  template <class F> void for_each_leaf(F f) const {
+    Cursor c = cursor_at_start();
+    Leaf* lf = c.node;
+    while (true) {
+      f(lf);
+      Cursor k{lf, lf->n ? lf->n - 1 : 0, 0};
+      if (!const_cast<Tree*>(this)->traverse(k, true)) break;
+      lf = k.node;
+    }
+  }
+};
+
+// order -> leaf.  Semantically the reference's SplitList (split_list/mod.rs) restricted to what
+// ListCRDT reads: marker_at(order) for item orders (doc.rs:101-107).  Stored as an interval map;
+// replace_range == SplitList::replace_range (:235-336).
+struct OrderIndex {
+  // Dense order -> leaf table; replace_range writes the notified run.  Orders that were never
+  // notified (delete orders) stay nullptr.
+  std::vector<Leaf*> v;
+  void replace_range(u32 start, u32 len, Leaf* leaf) {
+    if (len == 0) return;
+    if ((size_t)start + len > v.size()) v.resize(std::max<size_t>((size_t)start + len, v.size() * 2), nullptr);
+    std::fill(v.begin() + start, v.begin() + start + len, leaf);
+  }
+  Leaf* at(u32 order) const { return order < v.size() ? v[order] : nullptr; }
+};
+
+inline void Tree::notify(const Span& e, Leaf* leaf) {
+  if (track_index && index) index->replace_range(e.order, slen(e), leaf);
+}
+
+// ---------------------------------------------------------------------------------------------
+// RLE tables  (src/rle/simple_rle.rs, src/rle/mod.rs, order.rs, entry.rs, delete.rs,
+//              double_delete.rs, txn.rs)
+// ---------------------------------------------------------------------------------------------
+struct CwoRun { u32 key, agent, seq, len; };     // KVPair<CRDTSpan>   (client_with_order)
+struct IoRun { u32 key, order, len; };           // KVPair<OrderSpan>  (item_orders, len>0)
+struct DelRun { u32 key, order, len; };          // KVPair<DeleteEntry>
+struct DDRun { u32 key, len, excess; };          // KVPair<DoubleDelete>
+struct TxnRec { u32 order, len, shadow; std::vector<u32> parents; };  // TxnSpan
+
+// Rle::search comparator (simple_rle.rs:18-25); returns idx (>=0) or -(insert_pos)-1
+template <class V, class KeyF, class LenF>
+inline i64 rle_search(const std::vector<V>& v, u32 needle, KeyF key, LenF len) {
+  i64 lo = 0, hi = (i64)v.size();
+  while (lo < hi) {
+    i64 mid = (lo + hi) / 2;
+    u32 k = key(v[mid]);
+    if (needle < k) hi = mid;
+    else if (needle >= k + len(v[mid])) lo = mid + 1;
+    else return mid;
+  }
+  return -lo - 1;
+}
+
+// double_delete.rs:41-107 (increment_delete_range)
+inline void increment_delete_range(std::vector<DDRun>& v, u32 base, u32 len) {
+  DDRun next{base, len, 1};
+  i64 s = rle_search(v, base, [](const DDRun& r) { return r.key; }, [](const DDRun& r) { return r.len; });
+  size_t idx = s >= 0 ? (size_t)s : (size_t)(-s - 1);
+  auto dd_can_append = [](const DDRun& a, const DDRun& b) { return b.key == a.key + a.len && b.excess == a.excess; };
+  while (true) {
+    if (idx == v.size() || v[idx].key > next.key) {
+      DDRun here = next;
+      bool done_here;
+      if (idx < v.size() && next.key + next.len > v[idx].key) {
+        u32 at = v[idx].key - here.key;
+        next = DDRun{here.key + at, here.len - at, here.excess};
+        here.len = at;
+        done_here = false;
+      } else done_here = true;
+      if (idx >= 1 && dd_can_append(v[idx - 1], here)) v[idx - 1].len += here.len;
+      else { v.insert(v.begin() + idx, here); idx++; }
+      if (done_here) break;
+    }
+    DDRun& e = v[idx];
+    if (e.key < next.key) {
+      u32 at = next.key - e.key;
+      DDRun remd{e.key + at, e.len - at, e.excess};
+      e.len = at;
+      idx++;
+      v.insert(v.begin() + idx, remd);
+    }
+    DDRun& e2 = v[idx];
+    if (e2.len <= next.len) {
+      e2.excess += 1;
+      next.key += e2.len;
+      next.len -= e2.len;
+      if (next.len == 0) break;
+      idx++;
+    } else {
+      DDRun remd{e2.key + next.len, e2.len - next.len, e2.excess};
+      e2.len = next.len;
+      e2.excess += 1;
+      v.insert(v.begin() + idx + 1, remd);
+      break;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ListCRDT  (src/list/doc.rs, src/list/mod.rs)
+// ---------------------------------------------------------------------------------------------
+struct LocalOp { u32 pos, del, ins; };
+struct RemoteId { std::string agent; u32 seq; };
+struct RemoteOp { bool is_del; RemoteId a, b; u32 len; };  // Ins: a=origin_left b=origin_right
+struct RemoteTxn { RemoteId id; std::vector<RemoteId> parents; std::vector<RemoteOp> ops; };
+
+struct Client { std::string name; std::vector<IoRun> item_orders; };
+
+struct Stats { u64 q2_triggers = 0; u64 integrate_iters = 0; u64 leaves_max = 0; };
+
+struct Doc {
+  Tree tree;
+  OrderIndex index;
+  std::vector<CwoRun> cwo;
+  std::vector<Client> clients;
+  std::vector<DelRun> deletes;
+  std::vector<DDRun> double_deletes;
+  std::vector<TxnRec> txns;
+  std::vector<u32> frontier{ROOT_ORDER};
+  int status = OK;
+  Stats stats;
+
+  Doc(u32 L = 32, u32 NC = 16, bool track_index = true) : tree(L, NC) {
+    tree.index = &index;
+    tree.track_index = track_index;
+  }
+
+  // doc.rs:66-89
+  u16 get_or_create_agent_id(const std::string& name) {
+    if (name == "ROOT") return ROOT_AGENT;
+    int id = get_agent_id(name);
+    if (id >= 0) return (u16)id;
+    clients.push_back(Client{name, {}});
+    return (u16)(clients.size() - 1);
+  }
+  int get_agent_id(const std::string& name) const {
+    if (name == "ROOT") return ROOT_AGENT;
+    for (size_t i = 0; i < clients.size(); i++) if (clients[i].name == name) return (int)i;
+    return -1;
+  }
+  // doc.rs:20-24
+  u32 next_seq(u16 agent) const {
+    const auto& io = clients[agent].item_orders;
+    return io.empty() ? 0 : io.back().key + io.back().len;
+  }
+  // doc.rs:26-29
+  bool seq_to_order(u16 agent, u32 seq, u32& order) const {
+    const auto& io = clients[agent].item_orders;
+    i64 s = rle_search(io, seq, [](const IoRun& r) { return r.key; }, [](const IoRun& r) { return r.len; });
+    if (s < 0) return false;
+    order = io[s].order + (seq - io[s].key);
+    return true;
+  }
+  // doc.rs:95-99
+  u32 next_order() const { return cwo.empty() ? 0 : cwo.back().key + cwo.back().len; }
+  // client_with_order.get(order) (simple_rle.rs:98-103)
+  bool order_to_loc(u32 order, u16& agent, u32& seq) const {
+    i64 s = rle_search(cwo, order, [](const CwoRun& r) { return r.key; }, [](const CwoRun& r) { return r.len; });
+    if (s < 0) return false;
+    agent = (u16)cwo[s].agent;
+    seq = cwo[s].seq + (order - cwo[s].key);
+    return true;
+  }
+  // doc.rs:155-165
+  void assign_order_to_client(u16 agent, u32 seq, u32 order, u32 len) {
+    CwoRun r{order, agent, seq, len};
+    if (!cwo.empty()) {
+      CwoRun& l = cwo.back();
+      if (r.key == l.key + l.len && r.agent == l.agent && r.seq == l.seq + l.len) { l.len += len; goto io; }
+    }
+    cwo.push_back(r);
+  io:
+    auto& io = clients[agent].item_orders;
+    IoRun q{seq, order, len};
+    if (!io.empty()) {
+      IoRun& l = io.back();
+      if (q.key == l.key + l.len && ((i32)len > 0) == ((i32)l.len > 0) && q.order == l.order + l.len) { l.len += len; return; }
+    }
+    io.push_back(q);
+  }
+  // doc.rs:109-136
+  bool get_cursor_before(u32 order, Cursor& c) {
+    if (order == ROOT_ORDER) return tree.cursor_at_end(c);
+    Leaf* lf = index.at(order);
+    if (!lf) return false;
+    return Tree::leaf_find(lf, order, c);
+  }
+  bool get_cursor_after(u32 order, Cursor& c) {
+    if (order == ROOT_ORDER) { c = tree.cursor_at_start(); return true; }
+    if (!get_cursor_before(order, c)) return false;
+    c.off += 1;
+    return true;
+  }
+  void append_delete(u32 key, u32 target, u32 len) {  // Rle::append of KVPair<DeleteEntry>
+    if (!deletes.empty()) {
+      DelRun& l = deletes.back();
+      if (key == l.key + l.len && l.order + l.len == target) { l.len += len; return; }
+    }
+    deletes.push_back(DelRun{key, target, len});
+  }
+
+  // doc.rs:167-234.  Returns status.
+  int integrate(u16 agent, const Span& item, const Cursor* hint) {
+    Cursor cursor;
+    if (hint) cursor = *hint;
+    else if (!get_cursor_after(item.ol, cursor)) return ERR_UNKNOWN_ID;
+    Cursor left = cursor, scan_start = cursor;
+    bool scanning = false;
+    bool first = true;
+    while (true) {
+      u32 other_order;
+      if (!tree.get_item(cursor, other_order)) break;
+      if (other_order == item.orr) break;
+      stats.integrate_iters++;
+      Span other_entry = cursor.node->data[cursor.idx];
+      u32 other_left_order = origin_left_at_offset(other_entry, cursor.off);
+      Cursor olc;
+      if (!get_cursor_after(other_left_order, olc)) return ERR_UNKNOWN_ID;
+      int c = tree.cmp(olc, left);
+      if (c < 0) break;
+      if (c == 0) {
+        u16 oa; u32 os;
+        if (!order_to_loc(other_entry.order, oa, os)) return ERR_UNKNOWN_ID;
+        // Q2: the tie-break reads the agent of the entry's *first* order
+        u16 ia; u32 is_;
+        if (order_to_loc(other_order, ia, is_) && ia != oa) stats.q2_triggers++;
+        (void)first;
+        const std::string& my = clients[agent].name;
+        const std::string& other = clients[oa].name;
+        if (my > other) scanning = false;
+        else if (item.orr == other_entry.orr) break;
+        else { scanning = true; scan_start = cursor; }
+      }
+      first = false;
+      if (!tree.next_entry(cursor)) return ERR_NONTERMINATING;  // cursor unchanged => loops forever
+    }
+    if (scanning) cursor = scan_start;
+    tree.insert(cursor, item);
+    return OK;
+  }
+
+  // doc.rs:236-240
+  int remote_id_to_order(const RemoteId& id, u32& order) const {
+    int a = get_agent_id(id.agent);
+    if (a < 0) return ERR_UNKNOWN_AGENT;
+    if (a == ROOT_AGENT) { order = ROOT_ORDER; return OK; }
+    if (!seq_to_order((u16)a, id.seq, order)) return ERR_UNKNOWN_ID;
+    return OK;
+  }
+
+  // doc.rs:350-374 (+ advance_branch_by :34-48)
+  int insert_txn(const std::vector<u32>* remote_parents, u32 first_order, u32 len) {
+    u32 last_order = first_order + len - 1;
+    std::vector<u32> parents;
+    if (remote_parents) {
+      if (std::find(frontier.begin(), frontier.end(), first_order) != frontier.end()) return ERR_FRONTIER;
+      std::vector<u32> nf;
+      for (u32 o : frontier) if (std::find(remote_parents->begin(), remote_parents->end(), o) == remote_parents->end()) nf.push_back(o);
+      nf.push_back(last_order);
+      frontier = nf;
+      parents = *remote_parents;
+    } else {
+      parents = frontier;
+      frontier = {last_order};
+    }
+    u32 shadow = first_order;
+    while (shadow >= 1 && std::find(parents.begin(), parents.end(), shadow - 1) != parents.end()) {
+      i64 s = rle_search(txns, shadow - 1, [](const TxnRec& t) { return t.order; }, [](const TxnRec& t) { return t.len; });
+      if (s < 0) return ERR_UNKNOWN_ID;
+      shadow = txns[s].shadow;
+    }
+    TxnRec t{first_order, len, shadow, parents};
+    if (!txns.empty()) {
+      TxnRec& l = txns.back();
+      if (t.parents.size() == 1 && t.parents[0] == l.order + l.len - 1 && t.shadow == l.shadow) { l.len += len; return OK; }
+    }
+    txns.push_back(std::move(t));
+    return OK;
+  }
+
+  // doc.rs:376-469
+  int apply_local_txn(u16 agent, const LocalOp* ops, u32 nops) {
+    if (status != OK) return status;
+    if (agent == ROOT_AGENT || agent >= clients.size()) return status = ERR_UNKNOWN_AGENT;
+    u32 first_order = next_order();
+    u32 next = first_order;
+    u32 span = 0;
+    for (u32 i = 0; i < nops; i++) span += ops[i].del + ops[i].ins;
+    if (span == 0) return status = ERR_EMPTY_TXN;
+    assign_order_to_client(agent, next_seq(agent), first_order, span);
+    std::vector<Span> deleted;
+    for (u32 i = 0; i < nops; i++) {
+      u32 pos = ops[i].pos;
+      if (ops[i].del > 0) {
+        if ((u64)pos + ops[i].del > tree.count) return status = ERR_POS_OOB;
+        Cursor c;
+        if (!tree.cursor_at_content_pos(pos, c)) return status = ERR_POS_OOB;
+        deleted.clear();
+        if (!tree.local_deactivate(c, ops[i].del, deleted)) return status = ERR_POS_OOB;
+        u32 dl = 0;
+        for (const Span& it : deleted) {
+          append_delete(next, it.order, (u32)it.len);
+          dl += (u32)it.len;
+          next += (u32)it.len;
+        }
+        if (dl != ops[i].del) return status = ERR_POS_OOB;
+      }
+      if (ops[i].ins > 0) {
+        u32 order = next;
+        next += ops[i].ins;
+        u32 ol;
+        Cursor c;
+        if (pos == 0) { ol = ROOT_ORDER; c = tree.cursor_at_start(); }
+        else {
+          if (pos > tree.count) return status = ERR_POS_OOB;
+          if (!tree.cursor_at_content_pos(pos - 1, c)) return status = ERR_POS_OOB;
+          if (!tree.get_item(c, ol)) return status = ERR_POS_OOB;
+          if (!tree.next(c)) return status = ERR_POS_OOB;
+        }
+        u32 orr;
+        if (!tree.get_item(c, orr)) orr = ROOT_ORDER;
+        Span item{order, ol, orr, (i32)ops[i].ins};
+        int st = integrate(agent, item, &c);
+        if (st != OK) return status = st;
+      }
+    }
+    int st = insert_txn(nullptr, first_order, next - first_order);
+    if (st != OK) return status = st;
+    return OK;
+  }
+
+  // doc.rs:242-348
+  int apply_remote_txn(const RemoteTxn& txn) {
+    if (status != OK) return status;
+    u16 agent = get_or_create_agent_id(txn.id.agent);
+    if (agent == ROOT_AGENT) return status = ERR_UNKNOWN_AGENT;
+    if (next_seq(agent) != txn.id.seq) return status = ERR_SEQ;
+    u32 first_order = next_order();
+    u32 next = first_order;
+    u32 txn_len = 0;
+    for (const auto& op : txn.ops) {
+      if (op.len == 0) return status = ERR_BAD_INPUT;
+      txn_len += op.len;
+    }
+    if (txn_len == 0) return status = ERR_EMPTY_TXN;
+    assign_order_to_client(agent, txn.id.seq, first_order, txn_len);
+    for (const auto& op : txn.ops) {
+      if (!op.is_del) {
+        u32 order = next;
+        next += op.len;
+        u32 ol, orr;
+        int st = remote_id_to_order(op.a, ol);
+        if (st != OK) return status = st;
+        st = remote_id_to_order(op.b, orr);
+        if (st != OK) return status = st;
+        Span item{order, ol, orr, (i32)op.len};
+        st = integrate(agent, item, nullptr);
+        if (st != OK) return status = st;
+      } else {
+        u32 order = next;
+        next += op.len;
+        u32 target;
+        int st = remote_id_to_order(op.a, target);
+        if (st != OK) return status = st;
+        append_delete(order, target, op.len);
+        u32 remaining = op.len;
+        while (remaining > 0) {
+          if (target == ROOT_ORDER) return status = ERR_NONTERMINATING;  // cursor_at_end + 0-progress loop
+          Cursor c;
+          if (!get_cursor_before(target, c)) return status = ERR_UNKNOWN_ID;
+          i64 amt = tree.remote_deactivate(c, remaining);
+          u32 here = (u32)(amt < 0 ? -amt : amt);
+          if (here == 0) return status = ERR_NONTERMINATING;
+          if (amt < 0) increment_delete_range(double_deletes, target, here);
+          remaining -= here;
+          target += here;
+        }
+      }
+    }
+    std::vector<u32> parents;
+    for (const auto& p : txn.parents) {
+      u32 o;
+      int st = remote_id_to_order(p, o);
+      if (st != OK) return status = st;
+      parents.push_back(o);
+    }
+    int st = insert_txn(&parents, first_order, txn_len);
+    if (st != OK) return status = st;
+    return OK;
+  }
+
+  u32 len() const { return tree.count; }  // doc.rs:484-486
+
+  // --- exports used by parity checks -------------------------------------------------------
+  void raw_entries(std::vector<Span>& out, std::vector<u32>& leaf_sizes) const {
+    out.clear();
+    leaf_sizes.clear();
+    tree.for_each_leaf([&](Leaf* lf) {
+      leaf_sizes.push_back(lf->n);
+      for (u32 i = 0; i < lf->n; i++) out.push_back(lf->data[i]);
+    });
+  }
+  // greedy can_append coalescing of the item sequence (layout independent)
+  void canonical(std::vector<Span>& out) const {
+    out.clear();
+    tree.for_each_leaf([&](Leaf* lf) {
+      for (u32 i = 0; i < lf->n; i++) {
+        const Span& e = lf->data[i];
+        if (!out.empty() && can_append(out.back(), e)) append(out.back(), e);
+        else out.push_back(e);
+      }
+    });
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Digest (definition shared with the GPU digest kernel; see DESIGN.md "Digest")
+// ---------------------------------------------------------------------------------------------
+inline u64 mix64(u64 z) {  // splitmix64 finaliser
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline u64 elem_hash(u32 section, u64 idx, u64 a, u64 b) {
+  u64 k = mix64(((u64)section << 56) ^ idx);
+  return mix64(mix64(k ^ a) ^ b);
+}
+inline u64 digest(const Doc& d) {
+  std::vector<Span> canon;
+  d.canonical(canon);
+  u64 h = 0;
+  for (size_t i = 0; i < canon.size(); i++)
+    h += elem_hash(1, i, ((u64)canon[i].order << 32) | canon[i].ol, ((u64)canon[i].orr << 32) | (u32)canon[i].len);
+  for (size_t i = 0; i < d.cwo.size(); i++)
+    h += elem_hash(2, i, ((u64)d.cwo[i].key << 32) | d.cwo[i].agent, ((u64)d.cwo[i].seq << 32) | d.cwo[i].len);
+  for (size_t i = 0; i < d.deletes.size(); i++)
+    h += elem_hash(3, i, ((u64)d.deletes[i].key << 32) | d.deletes[i].order, d.deletes[i].len);
+  for (size_t i = 0; i < d.double_deletes.size(); i++)
+    h += elem_hash(4, i, ((u64)d.double_deletes[i].key << 32) | d.double_deletes[i].len, d.double_deletes[i].excess);
+  u64 pidx = 0;
+  for (size_t i = 0; i < d.txns.size(); i++) {
+    const TxnRec& t = d.txns[i];
+    h += elem_hash(5, i, ((u64)t.order << 32) | t.len, ((u64)t.shadow << 32) | (u32)t.parents.size());
+    for (u32 p : t.parents) h += elem_hash(6, pidx++, p, i);
+  }
+  for (size_t i = 0; i < d.frontier.size(); i++) h += elem_hash(7, i, d.frontier[i], 0);
+  u64 counts = elem_hash(8, 0, ((u64)d.len() << 32) | (u32)canon.size(), ((u64)d.cwo.size() << 32) | (u32)d.deletes.size());
+  counts ^= elem_hash(9, 0, ((u64)d.double_deletes.size() << 32) | (u32)d.txns.size(), ((u64)d.frontier.size() << 32) | pidx);
+  return mix64(h ^ counts);
+}
+
+}  // namespace orc

@@ -1,0 +1,223 @@
+"""Pin the oracle (CPU restatement) against the reference's own tests and fixtures.
+
+CPU-only.  Each test names the reference test / assertion it ports.
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle_lib import OracleDoc, DoubleDeletes, OK, ERR_POS_OOB, ERR_SEQ, ERR_NONTERMINATING
+from crdt_amd.traces import TRACE_NAMES, load_trace, load_remote_wire
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "oracle_golden.json")))
+ROOT_ID = ("ROOT", 0xFFFFFFFF)
+
+
+def wire(txns, names=None):
+    """Build a wire batch from [(agent, seq, [parents], [ops])]; op = ('ins', ol, or, len) | ('del', id, len)."""
+    import struct
+    names = list(names or [])
+
+    def ni(n):
+        if n not in names:
+            names.append(n)
+        return names.index(n)
+
+    body = []
+    for agent, seq, parents, ops in txns:
+        body += [ni(agent), seq, len(parents), len(ops)]
+        for p in parents:
+            body += [ni(p[0]), p[1]]
+        for op in ops:
+            if op[0] == "ins":
+                body += [0, ni(op[1][0]), op[1][1], ni(op[2][0]), op[2][1], op[3]]
+            else:
+                body += [1, ni(op[1][0]), op[1][1], 0, 0, op[2]]
+    out = struct.pack("<II", 0x31585452, len(names))
+    for n in names:
+        b = n.encode()
+        out += struct.pack("<I", len(b)) + b + b"\0" * ((4 - len(b) % 4) % 4)
+    out += struct.pack("<I", len(txns)) + np.array(body, dtype=np.uint32).tobytes()
+    return out
+
+
+# --- double_delete.rs:114-139 inc_delete_range (exact golden vectors) -------------------------
+def test_inc_delete_range():
+    d = DoubleDeletes()
+    d.increment(5, 3)
+    assert d.get() == [(5, 3, 1)]
+    d.increment(5, 3)
+    assert d.get() == [(5, 3, 2)]
+    d.increment(4, 2)
+    assert d.get() == [(4, 1, 1), (5, 1, 3), (6, 2, 2)]
+    d.increment(7, 3)
+    assert d.get() == [(4, 1, 1), (5, 1, 3), (6, 1, 2), (7, 1, 3), (8, 2, 1)]
+
+
+# --- benches/yjs.rs:39,46: final doc.len() == endContent.len() --------------------------------
+@pytest.mark.parametrize("name", TRACE_NAMES)
+@pytest.mark.parametrize("caps", [(32, 16), (4, 8)])
+def test_trace_final_length(name, caps):
+    t = load_trace(name)
+    assert t.start_len == 0
+    d = OracleDoc(*caps)
+    assert d.apply_trace(d.agent("jeremy"), t.counts, t.patches) == OK
+    assert len(d) == t.end_len
+    g = GOLDEN[f"{name}/L{caps[0]}"]
+    assert g["len"] == t.end_len
+    assert hex(d.digest()) == g["digest"]
+    assert d.sizes() == g["sizes"]
+
+
+# --- doc.rs:620-676 remote_txns (remote == local for frontier/txns/deletes), whole traces ------
+@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode"])
+def test_remote_replay_equals_local(name):
+    t = load_trace(name)
+    loc = OracleDoc()
+    loc.apply_trace(loc.agent("jeremy"), t.counts, t.patches)
+    rem = OracleDoc()
+    assert rem.apply_remote_wire(load_remote_wire(name)) == OK
+    el, er = loc.export(), rem.export()
+    for k in ("raw", "leaf_sizes", "cwo", "deletes", "txns", "parents", "frontier"):
+        assert np.array_equal(el[k], er[k]), k
+    assert loc.digest() == rem.digest() == int(GOLDEN[f"{name}/L32"]["remote_digest"], 16)
+
+
+def test_remote_txns_unit():
+    # The exact reference test: seph@0 Ins "hi" (ROOT, ROOT), then seph@2 Del(seph@0, 2).
+    rem = OracleDoc(4, 8)
+    assert rem.apply_remote_wire(wire([("seph", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 2)])])) == OK
+    loc = OracleDoc(4, 8)
+    loc.agent("seph")
+    assert loc.local_insert(0, 0, 2) == OK
+    a, b = rem.export(), loc.export()
+    for k in ("frontier", "txns", "parents", "deletes"):
+        assert np.array_equal(a[k], b[k]), k
+    assert rem.apply_remote_wire(wire([("seph", 2, [("seph", 1)], [("del", ("seph", 0), 2)])])) == OK
+    assert loc.local_delete(0, 0, 2) == OK
+    a, b = rem.export(), loc.export()
+    for k in ("frontier", "txns", "parents", "deletes"):
+        assert np.array_equal(a[k], b[k]), k
+    assert len(rem) == len(loc) == 0
+
+
+# --- doc.rs:522-532 smoke ---------------------------------------------------------------------
+def test_smoke():
+    d = OracleDoc(4, 8)
+    a = d.agent("seph")
+    assert d.local_insert(a, 0, 2) == OK     # "hi"
+    assert d.local_insert(a, 1, 4) == OK     # "hyoooi"
+    assert d.local_delete(a, 0, 3) == OK     # "ooi"
+    assert len(d) == 3
+
+
+# --- doc.rs:589-601 deletes_merged --------------------------------------------------------------
+def test_deletes_merged():
+    d = OracleDoc(4, 8)
+    a = d.agent("seph")
+    d.local_insert(a, 0, 3)
+    for _ in range(3):
+        assert d.local_delete(a, 0, 1) == OK
+    e = d.export()
+    assert len(d) == 0
+    assert e["deletes"].tolist() == [[3, 0, 3]]   # three single deletes coalesce (Rle::append)
+    m = 0xFFFFFFFF
+    assert e["raw"][:, 3].tolist() == [-1 & m] * 3        # the tree keeps three deleted entries
+    assert e["canon"].tolist() == [[0, m, m, -3 & m]]     # which are one item-level run
+
+
+# --- doc.rs:571-587 random_single_document (own RNG; SmallRng seed-7 stream is Rust-only) -----
+def make_random_change(d, a, rng, shadow):
+    n = len(d)
+    w = 0.55 if n < 100 else 0.45
+    if n == 0 or rng.random() < w:
+        pos = rng.randint(0, n)
+        assert d.local_insert(a, pos, 1) == OK
+        shadow.insert(pos, "x")
+    else:
+        pos = rng.randint(0, n - 1)
+        span = rng.randint(1, min(10, n - pos))
+        assert d.local_delete(a, pos, span) == OK
+        del shadow[pos:pos + span]
+
+
+@pytest.mark.parametrize("caps", [(32, 16), (4, 8)])
+def test_random_single_document(caps):
+    rng = random.Random(7)
+    d = OracleDoc(*caps)
+    a = d.agent("seph")
+    shadow = []
+    for _ in range(1000):
+        make_random_change(d, a, rng, shadow)
+        assert len(d) == len(shadow)
+    s = d.sizes()
+    assert s["cwo"] == 1 and s["agents"] == 1      # client_with_order / item_orders: 1 entry
+    assert s["txns"] == 1
+
+
+# --- error paths mirror the reference's panics -----------------------------------------------
+def test_errors():
+    d = OracleDoc()
+    a = d.agent("seph")
+    assert d.local_insert(a, 1, 1) == ERR_POS_OOB           # root.rs:71/79 panic
+    d = OracleDoc()
+    a = d.agent("seph")
+    d.local_insert(a, 0, 5)
+    assert d.local_delete(a, 3, 3) == ERR_POS_OOB           # mutations.rs:573 panic
+    r = OracleDoc()
+    assert r.apply_remote_wire(wire([("seph", 1, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 1)])])) == ERR_SEQ
+
+
+def test_concurrent_nontermination_detected():
+    # A types "ab" (one entry); B inserts after 'a' concurrently (origin_right ROOT).  The
+    # reference's integrate lands mid-entry in the last entry of the doc and next_entry() fails
+    # without moving the cursor (cursor.rs:127-141) -> the loop never exits (doc.rs:183-221).
+    d = OracleDoc()
+    w = wire([("A", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 2)]),
+              ("B", 0, [("A", 0)], [("ins", ("A", 0), ROOT_ID, 1)])])
+    assert d.apply_remote_wire(w) == ERR_NONTERMINATING
+
+
+def test_concurrent_at_doc_end_is_nonterminating():
+    # Two agents insert at the start of a 1-item document concurrently: the scan reaches the last
+    # entry of the document and next_entry() cannot advance -> the reference loops forever.
+    w1 = [("A", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 1)]), ("B", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 1)])]
+    d1, d2 = OracleDoc(), OracleDoc()
+    assert d1.apply_remote_wire(wire(w1)) == ERR_NONTERMINATING
+    assert d2.apply_remote_wire(wire(w1[::-1])) == OK   # A sorts before B: breaks on origin_right
+
+
+def test_concurrent_tiebreak_converges():
+    # base "xy" by X; A and B both insert between x and y concurrently.  Both delivery orders
+    # give x A B y (doc.rs:204-216 name tie-break, incl. the end-of-entry first iteration).
+    base = ("X", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 2)])
+    ta = ("A", 0, [("X", 1)], [("ins", ("X", 0), ("X", 1), 1)])
+    tb = ("B", 0, [("X", 1)], [("ins", ("X", 0), ("X", 1), 1)])
+    res = []
+    for order in ((base, ta, tb), (base, tb, ta)):
+        d = OracleDoc()
+        assert d.apply_remote_wire(wire(list(order))) == OK
+        names = [t[0] for t in order]
+        ag, sq = d.pos_to_loc(np.arange(4))
+        res.append([(names[a], int(q)) for a, q in zip(ag, sq)])
+    assert res[0] == res[1] == [("X", 0), ("A", 0), ("B", 0), ("X", 1)]
+
+
+def test_queries_roundtrip():
+    t = load_trace("sveltecomponent")
+    d = OracleDoc()
+    d.apply_trace(d.agent("jeremy"), t.counts, t.patches)
+    pos = np.arange(len(d), dtype=np.uint32)
+    ag, seq = d.pos_to_loc(pos)
+    assert (ag == 0).all()
+    p2, dl = d.loc_to_pos(ag, seq)
+    assert np.array_equal(p2, pos) and (dl == 0).all()
+    # every seq: deleted items map to the position of the next visible item
+    allseq = np.arange(d.sizes()["next_order"], dtype=np.uint32)
+    p3, dl3 = d.loc_to_pos(np.zeros_like(allseq, dtype=np.uint16), allseq)
+    assert ((dl3 == 0) | (dl3 == 1) | (dl3 == 2)).all()
+    assert (p3[dl3 != 2] <= len(d)).all()

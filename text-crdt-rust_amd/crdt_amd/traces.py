@@ -1,0 +1,67 @@
+"""Trace ingestion: the repo's compact binary form of the reference's editing traces.
+
+Mirrors crdt-testdata's `load_testing_data` (src/testdata/src/lib.rs:29-48): a trace is a list of
+txns, each a list of patches (pos, del_len, ins_content); positions count Unicode scalar values.
+The JSON->binary conversion is tests/golden/make_traces.py (run once in the build container).
+Only lengths of inserted strings are used by the CRDT hot path (doc.rs:383: chars().count()).
+"""
+from __future__ import annotations
+
+import gzip
+import os
+import struct
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+DATA_DIR = os.path.normpath(os.path.join(_HERE, "..", "..", "data", "traces"))
+TRACE_NAMES = ("automerge-paper", "rustcode", "sveltecomponent")
+
+
+@dataclass
+class Trace:
+    name: str
+    counts: np.ndarray      # u32[n_txns]   patches per txn
+    patches: np.ndarray     # u32[n_patches, 3]  (pos, del_len, ins_len)
+    start_len: int
+    end_len: int            # chars of endContent
+    end_bytes: int
+    end_fnv: int
+    text: bytes             # all inserted strings, utf-8, concatenated
+
+    @property
+    def n_txns(self) -> int:
+        return int(self.counts.shape[0])
+
+    @property
+    def n_patches(self) -> int:
+        return int(self.patches.shape[0])
+
+    @property
+    def n_orders(self) -> int:
+        return int(self.patches[:, 1].sum() + self.patches[:, 2].sum())
+
+
+def load_trace(name: str, data_dir: str = DATA_DIR) -> Trace:
+    path = os.path.join(data_dir, name + ".trc.gz")
+    with gzip.open(path, "rb") as f:
+        blob = f.read()
+    if blob[:8] != b"CRDTTRC1":
+        raise ValueError(f"{path}: bad magic")
+    n_txns, n_patches, start_len, end_len, end_bytes, end_fnv = struct.unpack_from("<5IQ", blob, 8)
+    off = 8 + 28
+    counts = np.frombuffer(blob, dtype=np.uint32, count=n_txns, offset=off).copy()
+    off += 4 * n_txns
+    patches = np.frombuffer(blob, dtype=np.uint32, count=3 * n_patches, offset=off).reshape(n_patches, 3).copy()
+    off += 12 * n_patches
+    (tb,) = struct.unpack_from("<I", blob, off)
+    text = blob[off + 4: off + 4 + tb]
+    return Trace(name, counts, patches, start_len, end_len, end_bytes, end_fnv, text)
+
+
+def load_remote_wire(name: str, data_dir: str = DATA_DIR) -> bytes:
+    """Remote-form (RemoteTxn wire batch) of a trace, generated offline by
+    tests/golden/make_remote.py (see include/crdt_gpu.h "Remote wire batch")."""
+    with gzip.open(os.path.join(data_dir, name + ".rtx.gz"), "rb") as f:
+        return f.read()
