@@ -1,0 +1,248 @@
+// TEST INFRASTRUCTURE: runs replay_core.h on the CPU (WaveCPU backend) for single documents,
+// using the same host planning code as the engine, and exports the resulting state in the
+// oracle's export format so tests can diff the GPU algorithm against the oracle without a GPU.
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "host_plan.h"
+#include "replay_core.h"
+#include "wave_cpu.h"
+
+using namespace crdt;
+
+namespace {
+
+struct EmuDoc {
+  u32 L;
+  AgentTable agents;
+  std::vector<Span> leaves;
+  std::vector<u32> dir_leaf, dir_vis, sol, leaf_of, parents, frontier;
+  std::vector<CwoRun> cwo;
+  std::vector<ARun> arun;
+  std::vector<DelRun> dels;
+  std::vector<DDRun> dd;
+  std::vector<TxnRec> txns;
+  std::vector<AgentRec> agent_tab;
+  std::vector<GroupRec> groups;
+  std::vector<Rec> recs;
+  DocSeg seg{};
+  DocState st{};
+  bool inited = false;
+
+  Pools pools() {
+    Pools p{};
+    p.leaves = leaves.data();
+    p.dir_leaf = dir_leaf.data();
+    p.dir_vis = dir_vis.data();
+    p.slot_of_leaf = sol.data();
+    p.leaf_of = leaf_of.data();
+    p.cwo = cwo.data();
+    p.arun = arun.data();
+    p.dels = dels.data();
+    p.dd = dd.data();
+    p.txns = txns.data();
+    p.parents = parents.data();
+    p.frontier = frontier.data();
+    p.agents = agent_tab.data();
+    p.groups = groups.data();
+    p.recs = recs.data();
+    p.seg = &seg;
+    p.st = &st;
+    return p;
+  }
+
+  // (Re)allocate for a stream; a fresh document only (emulator scope).
+  void prepare(const StreamNeeds& nd, bool track, u32 leaf_div) {
+    Caps c = plan_caps(nd, (u32)agents.names.size(), track, leaf_div);
+    leaves.assign((size_t)c.leaf * L, Span{0, 0, 0, 0});
+    sol.assign(c.leaf, 0);
+    dir_leaf.assign((size_t)c.blk * GROUP, 0);
+    dir_vis.assign((size_t)c.blk * GROUP, 0);
+    leaf_of.assign(std::max<u32>(c.map, 1), 0xDEADBEEFu);
+    cwo.assign(c.cwo, CwoRun{});
+    arun.assign(c.arun, ARun{});
+    dels.assign(c.del, DelRun{});
+    dd.assign(c.dd, DDRun{});
+    txns.assign(c.txn, TxnRec{});
+    parents.assign(c.par, 0);
+    frontier.assign(FRONTIER_CAP, 0);
+    groups.assign(MAX_GROUPS, GroupRec{});
+    agent_tab.assign(std::max<u32>(c.agent, 1), AgentRec{});
+    std::vector<u32> rk = agents.ranks();
+    u32 base = 0;
+    for (u32 a = 0; a < agents.names.size(); a++) {
+      u32 cap = (a < nd.txns_per_agent.size() ? nd.txns_per_agent[a] : 0) + 1;
+      agent_tab[a] = AgentRec{base, 0, cap, rk[a]};
+      base += cap;
+    }
+    seg = DocSeg{};
+    seg.leaf_cap = c.leaf; seg.blk_cap = c.blk; seg.map_cap = c.map; seg.cwo_cap = c.cwo;
+    seg.arun_cap = c.arun; seg.del_cap = c.del; seg.dd_cap = c.dd; seg.txn_cap = c.txn;
+    seg.par_cap = c.par; seg.agent_cap = c.agent; seg.rec_n = (u32)recs.size();
+    seg.flags = track ? DOC_TRACK_MAP : 0;
+    st = DocState{};
+    st.n_agents = (u32)agents.names.size();
+  }
+
+  u32 grow_events = 0, grow_mask = 0;
+
+  // Grow the tables named by cap_need (the engine does the same on the device pools).
+  void grow(u32 need) {
+    grow_events++;
+    grow_mask |= need;
+    if (need & 1u) {
+      u32 nl = seg.leaf_cap * 2 > MAX_LEAVES ? MAX_LEAVES : seg.leaf_cap * 2;
+      leaves.resize((size_t)nl * L, Span{0, 0, 0, 0});
+      sol.resize(nl, 0);
+      seg.leaf_cap = nl;
+      seg.blk_cap = nl / 32 + 2;
+      dir_leaf.resize((size_t)seg.blk_cap * GROUP, 0);
+      dir_vis.resize((size_t)seg.blk_cap * GROUP, 0);
+    }
+    if (need & 2u) { seg.cwo_cap *= 2; seg.txn_cap *= 2; cwo.resize(seg.cwo_cap); txns.resize(seg.txn_cap); }
+    if (need & 4u) { seg.del_cap = seg.del_cap * 2 + 16; dels.resize(seg.del_cap); }
+    if (need & 8u) { seg.par_cap = seg.par_cap * 2 + 16; parents.resize(seg.par_cap); }
+    if (need & 16u) { seg.map_cap = seg.map_cap * 2 + 16; leaf_of.resize(seg.map_cap, 0xDEADBEEFu); }
+    if (need & 32u) {  // re-space every agent's run list with doubled capacity
+      std::vector<ARun> na;
+      for (u32 a = 0; a < st.n_agents; a++) {
+        AgentRec& A = agent_tab[a];
+        u32 base = (u32)na.size();
+        for (u32 k = 0; k < A.run_cnt; k++) na.push_back(arun[A.run_base + k]);
+        na.resize(base + A.run_cap * 2 + 1);
+        A.run_base = base;
+        A.run_cap = A.run_cap * 2 + 1;
+      }
+      arun = na;
+    }
+  }
+
+  template <int LL> int run_impl() {
+    bool first = true;
+    while (true) {
+      Pools p = pools();
+      WaveCPU<LL> w;
+      Replayer<WaveCPU<LL>, LL> r(w, p, 0);
+      if (first) { r.init_empty(); r.s.n_agents = (u32)agents.names.size(); first = false; }
+      else { r.s.status = ST_OK; r.begin(); }
+      r.run();
+      r.finish();
+      if (st.status != ST_NEED_CAPACITY) break;
+      if (st.cap_need == 0 || ((st.cap_need & 1u) && seg.leaf_cap >= MAX_LEAVES) || grow_events > 64) {
+        st.status = ST_CAPACITY;  // cannot grow further
+        break;
+      }
+      grow(st.cap_need);
+    }
+    return st.status;
+  }
+  int run() { return L == 32 ? run_impl<32>() : run_impl<4>(); }
+
+  // walk the directory in document order
+  void raw(std::vector<Span>& out, std::vector<u32>& leaf_sizes) const {
+    out.clear();
+    leaf_sizes.clear();
+    for (u32 g = 0; g < st.ng; g++) {
+      const GroupRec& G = groups[g];
+      for (u32 i = 0; i < G.cnt; i++) {
+        u32 lf = dir_leaf[(size_t)G.blk * GROUP + i];
+        u32 n = 0;
+        for (u32 k = 0; k < L; k++) if (leaves[(size_t)lf * L + k].len != 0) { out.push_back(leaves[(size_t)lf * L + k]); n++; }
+        leaf_sizes.push_back(n);
+      }
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+void* emu_new(uint32_t leaf_cap) {
+  if (leaf_cap != 4 && leaf_cap != 32) return nullptr;
+  EmuDoc* d = new EmuDoc();
+  d->L = leaf_cap;
+  return d;
+}
+void emu_free(void* h) { delete (EmuDoc*)h; }
+int emu_agent(void* h, const char* name) { return (int)((EmuDoc*)h)->agents.get_or_create(name); }
+
+// Apply a local trace (as one stream) to a fresh emulated document.
+int emu_run_local(void* h, uint16_t agent, uint32_t ntxn, const uint32_t* counts, const uint32_t* patches3, uint32_t leaf_div) {
+  EmuDoc* d = (EmuDoc*)h;
+  StreamNeeds nd;
+  d->recs.clear();
+  const uint32_t* p = patches3;
+  for (uint32_t t = 0; t < ntxn; t++) { encode_local_txn(d->recs, nd, agent, p, counts[t]); p += 3 * counts[t]; }
+  d->prepare(nd, true, leaf_div);
+  return d->run();
+}
+
+int emu_run_wire(void* h, const uint8_t* wire, size_t len, uint32_t leaf_div) {
+  EmuDoc* d = (EmuDoc*)h;
+  WireView wv;
+  if (!wv.parse(wire, len)) return ST_BAD_INPUT;
+  StreamNeeds nd;
+  d->recs.clear();
+  encode_remote(d->recs, nd, d->agents, wv);
+  d->prepare(nd, true, leaf_div);
+  return d->run();
+}
+
+// sizes: [n_raw, n_leaves, n_cwo, n_del, n_dd, n_txn, n_parents, n_frontier, n_agents, next_order, len, rec_pos]
+void emu_sizes(void* h, uint64_t* s) {
+  EmuDoc* d = (EmuDoc*)h;
+  std::vector<Span> raw;
+  std::vector<u32> ls;
+  d->raw(raw, ls);
+  s[0] = raw.size(); s[1] = ls.size(); s[2] = d->st.n_cwo; s[3] = d->st.n_del; s[4] = d->st.n_dd;
+  s[5] = d->st.n_txn; s[6] = d->st.n_par; s[7] = d->st.n_fr; s[8] = d->st.n_agents; s[9] = d->st.next_order;
+  s[10] = d->st.len; s[11] = d->st.rec_pos; s[12] = d->grow_events; s[13] = d->grow_mask;
+}
+
+void emu_export(void* h, uint32_t* raw4, uint32_t* leaf_sizes, uint32_t* cwo4, uint32_t* del3, uint32_t* dd3,
+                uint32_t* txn5, uint32_t* parents, uint32_t* frontier) {
+  EmuDoc* d = (EmuDoc*)h;
+  std::vector<Span> raw;
+  std::vector<u32> ls;
+  d->raw(raw, ls);
+  std::memcpy(raw4, raw.data(), raw.size() * 16);
+  std::memcpy(leaf_sizes, ls.data(), ls.size() * 4);
+  std::memcpy(cwo4, d->cwo.data(), d->st.n_cwo * 16);
+  std::memcpy(del3, d->dels.data(), d->st.n_del * 12);
+  std::memcpy(dd3, d->dd.data(), d->st.n_dd * 12);
+  for (u32 i = 0; i < d->st.n_txn; i++) {
+    const TxnRec& t = d->txns[i];
+    txn5[5 * i] = t.order; txn5[5 * i + 1] = t.len; txn5[5 * i + 2] = t.shadow; txn5[5 * i + 3] = t.poff; txn5[5 * i + 4] = t.pn;
+  }
+  std::memcpy(parents, d->parents.data(), d->st.n_par * 4);
+  std::memcpy(frontier, d->frontier.data(), d->st.n_fr * 4);
+}
+
+// Structural invariants of the wave directory (the analogue of RangeTree::check, root.rs:165-253).
+// Returns 0 if consistent, else a code and writes a message.
+int emu_check(void* h, char* msg, int cap) {
+  EmuDoc* d = (EmuDoc*)h;
+  u64 total = 0;
+  for (u32 g = 0; g < d->st.ng; g++) {
+    const GroupRec& G = d->groups[g];
+    u64 gsum = 0;
+    for (u32 i = 0; i < G.cnt; i++) {
+      u32 lf = d->dir_leaf[(size_t)G.blk * GROUP + i];
+      u32 dv = d->dir_vis[(size_t)G.blk * GROUP + i];
+      u32 v = 0;
+      for (u32 k = 0; k < d->L; k++) v += clen(d->leaves[(size_t)lf * d->L + k]);
+      if (v != dv) { snprintf(msg, cap, "group %u slot %u leaf %u: dir_vis %u content %u", g, i, lf, dv, v); return 1; }
+      if (d->sol[lf] != ((G.blk << 6) | i)) { snprintf(msg, cap, "slot_of_leaf[%u]=%x expected blk %u i %u", lf, d->sol[lf], G.blk, i); return 2; }
+      gsum += dv;
+    }
+    if (gsum != G.vis) { snprintf(msg, cap, "group %u vis %u sum %llu", g, G.vis, (unsigned long long)gsum); return 3; }
+    total += gsum;
+  }
+  if (total != d->st.len) { snprintf(msg, cap, "len %u total %llu", d->st.len, (unsigned long long)total); return 4; }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,147 @@
+// TEST INFRASTRUCTURE: a sequential CPU emulation of the WaveGPU backend, so replay_core.h's
+// control logic can be run (and debugged under ASan/gdb) against the oracle without a GPU.
+// Each method is the plain-loop meaning of the matching lane-parallel WaveGPU method.
+// Never linked into the product library.
+#pragma once
+#include <cstring>
+
+#include "crdt_types.h"
+
+namespace crdt {
+
+template <int L>
+struct WaveCPU {
+  Span c[64];
+  u32 gb[MAX_GROUPS], gc[MAX_GROUPS], gv[MAX_GROUPS];
+
+  WaveCPU() { std::memset(c, 0, sizeof(c)); std::memset(gb, 0, sizeof(gb)); std::memset(gc, 0, sizeof(gc)); std::memset(gv, 0, sizeof(gv)); }
+
+  u32 ld(const u32* p) const { return *p; }
+  void st(u32* p, u32 v) const { *p = v; }
+  void st(i32* p, i32 v) const { *p = v; }
+  template <class T> T ldT(const T* p) const { return *p; }
+  template <class T> void stT(T* p, const T& v) const { *p = v; }
+  AgentRec ld_agent(const AgentRec* p) const { return *p; }
+  ARun ld_arun(const ARun* p) const { return *p; }
+  void st_arun(ARun* p, const ARun& v) const { *p = v; }
+  CwoRun ld_cwo(const CwoRun* p) const { return *p; }
+  void st_cwo(CwoRun* p, const CwoRun& v) const { *p = v; }
+  DelRun ld_del(const DelRun* p) const { return *p; }
+  void st_del(DelRun* p, const DelRun& v) const { *p = v; }
+  DDRun ld_dd(const DDRun* p) const { return *p; }
+  void st_dd(DDRun* p, const DDRun& v) const { *p = v; }
+  TxnRec ld_txn(const TxnRec* p) const { return *p; }
+  void st_txn(TxnRec* p, const TxnRec& v) const { *p = v; }
+  Rec ld_rec(const Rec* p) const { return *p; }
+  void st_state(DocState* p, const DocState& s) const { *p = s; }
+  void fill(u32* p, u32 n, u32 v) const { for (u32 k = 0; k < n; k++) p[k] = v; }
+  void zero_leaf(Span* p, u32 n) const { std::memset(p, 0, sizeof(Span) * n); }
+
+  template <class T> static u32 rkey(const T& r) { return ((const u32*)&r)[0]; }
+  static u32 rlen(const ARun& r) { return r.len; }
+  static u32 rlen(const CwoRun& r) { return r.len; }
+  static u32 rlen(const DDRun& r) { return r.len; }
+  static u32 rlen(const TxnRec& r) { return r.len; }
+  template <class T> i32 search(const T* b, u32 n, u32 x) const {  // simple_rle.rs:18-25
+    u32 lo = 0, hi = n;
+    while (lo < hi) {
+      u32 mid = (lo + hi) / 2;
+      u32 k = rkey(b[mid]);
+      if (x < k) hi = mid;
+      else if (x >= k + rlen(b[mid])) lo = mid + 1;
+      else return (i32)mid;
+    }
+    return -1;
+  }
+  i32 search_arun(const ARun* b, u32 n, u32 x) const { return search(b, n, x); }
+  i32 search_cwo(const CwoRun* b, u32 n, u32 x) const { return search(b, n, x); }
+  i32 search_dd(const DDRun* b, u32 n, u32 x) const { return search(b, n, x); }
+  i32 search_txn(const TxnRec* b, u32 n, u32 x) const { return search(b, n, x); }
+
+  // leaf cache
+  u32 cache_load(const Span* p) {
+    u32 n = 0;
+    for (u32 i = 0; i < 64; i++) c[i] = i < (u32)L ? p[i] : Span{0, 0, 0, 0};
+    for (u32 i = 0; i < (u32)L; i++) n += c[i].len != 0;
+    return n;
+  }
+  void cache_store(Span* p, u32) const { for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
+  Span cget(u32 i) const { return c[i & 63]; }
+  void cset(u32 i, const Span& s) { c[i & 63] = s; }
+  u32 cache_vis(u32 a, u32 b) const { u32 t = 0; for (u32 i = a; i < b && i < 64; i++) t += clen(c[i]); return t; }
+  bool cfind_content(u32 n, u32 rem, u32& idx, u32& off) const {
+    for (u32 i = 0; i < n; i++) {
+      u32 e = clen(c[i]);
+      if (rem < e) { idx = i; off = rem; return true; }
+      rem -= e;
+    }
+    if (rem == 0) { idx = n; off = 0; return true; }
+    return false;
+  }
+  i32 cfind_order(u32 n, u32 order) const {
+    for (u32 i = 0; i < n; i++) if (order >= c[i].order && order - c[i].order < slen(c[i])) return (i32)i;
+    return -1;
+  }
+  void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) const {
+    for (u32 j = 0; j < (u32)L; j++) {
+      u32 src = j + idx - padding;
+      dst[j] = (j >= padding && src < n) ? c[src] : Span{0, 0, 0, 0};
+    }
+  }
+  void cache_clear(u32 a, u32 b) { for (u32 i = a; i < b; i++) c[i] = Span{0, 0, 0, 0}; }
+  void cache_shift_right(u32 idx, u32 n, u32 k) {
+    for (i32 i = (i32)n - 1; i >= (i32)idx; i--) c[i + k] = c[i];
+  }
+
+  // directory root
+  void root_init(u32 blk, u32 cnt, u32 vis) {
+    std::memset(gb, 0, sizeof(gb)); std::memset(gc, 0, sizeof(gc)); std::memset(gv, 0, sizeof(gv));
+    gb[0] = blk; gc[0] = cnt; gv[0] = vis;
+  }
+  void root_load(const GroupRec* g, u32 ng) { for (u32 i = 0; i < ng; i++) { gb[i] = g[i].blk; gc[i] = g[i].cnt; gv[i] = g[i].vis; } }
+  void root_store(GroupRec* g, u32 ng) const { for (u32 i = 0; i < ng; i++) g[i] = GroupRec{gb[i], gc[i], gv[i], 0}; }
+  u32 root_blk(u32 g) const { return gb[g]; }
+  u32 root_cnt(u32 g) const { return gc[g]; }
+  u32 root_vis(u32 g) const { return gv[g]; }
+  u32 root_find_blk(u32 ng, u32 blk) const { for (u32 i = 0; i < ng; i++) if (gb[i] == blk) return i; return INVALID; }
+  void root_add_vis(u32 g, u32 d) { gv[g] += d; }
+  void root_set(u32 g, u32 blk, u32 cnt, u32 vis) { gb[g] = blk; gc[g] = cnt; gv[g] = vis; }
+  void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
+    for (u32 i = ng; i > g; i--) { gb[i] = gb[i - 1]; gc[i] = gc[i - 1]; gv[i] = gv[i - 1]; }
+    root_set(g, blk, cnt, vis);
+  }
+  bool root_find_pos(u32 ng, u32 pos, u32& g, u32& base) const {
+    u32 acc = 0;
+    for (u32 i = 0; i < ng; i++) {
+      if (pos < acc + gv[i]) { g = i; base = acc; return true; }
+      acc += gv[i];
+    }
+    return false;
+  }
+  bool blk_find_pos(const u32* dv, u32 cnt, u32 rem, u32& i, u32& before) const {
+    u32 acc = 0;
+    for (u32 k = 0; k < cnt; k++) {
+      if (rem < acc + dv[k]) { i = k; before = acc; return true; }
+      acc += dv[k];
+    }
+    return false;
+  }
+  void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+    for (u32 k = cnt; k > i; k--) { dl[k] = dl[k - 1]; dv[k] = dv[k - 1]; }
+    dl[i] = leaf;
+    dv[i] = vis;
+    for (u32 k = i; k <= cnt; k++) sol[dl[k]] = (blk << 6) | k;
+  }
+  u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
+    u32 t = 0;
+    for (u32 k = 32; k < 64; k++) {
+      ndl[k - 32] = dl[k];
+      ndv[k - 32] = dv[k];
+      sol[dl[k]] = (nb << 6) | (k - 32);
+      t += dv[k];
+    }
+    return t;
+  }
+};
+
+}  // namespace crdt

@@ -1,0 +1,147 @@
+// Shared device/host types for the MI355X list-CRDT engine.
+//
+// Reference mapping (josephg/text-crdt-rust):
+//   Span        == YjsSpan                         src/list/span.rs:5-119
+//   CwoRun      == KVPair<CRDTSpan> (client_with_order)   src/list/mod.rs:63, range_tree/entry.rs:43-129
+//   ARun        == KVPair<OrderSpan> (ClientData::item_orders)  mod.rs:42, order.rs:6-104
+//   DelRun      == KVPair<DeleteEntry>             list/delete.rs:6-40
+//   DDRun       == KVPair<DoubleDelete>            list/double_delete.rs:11-38
+//   TxnRec      == TxnSpan (+ parents in a pool)   list/txn.rs:9-60
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace crdt {
+
+typedef uint8_t u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef int32_t i32;
+typedef uint64_t u64;
+typedef int64_t i64;
+
+#define CRDT_HD __host__ __device__ __forceinline__
+
+constexpr u32 ROOT_ORDER = 0xFFFFFFFFu;   // list/mod.rs:30
+constexpr u32 ROOT_AGENT = 0xFFFFu;       // "ROOT" -> AgentId::MAX (doc.rs:68)
+constexpr u32 UNKNOWN_AGENT = 0xFFFEu;    // a name that is not (yet) interned for this document
+constexpr u32 INVALID = 0xFFFFFFFFu;
+
+constexpr u32 GROUP = 64;                 // directory slots per block (one wavefront)
+constexpr u32 MAX_GROUP_REGS = 4;         // root level: up to 4 x 64 groups in VGPRs
+constexpr u32 MAX_GROUPS = GROUP * MAX_GROUP_REGS;
+constexpr u32 FRONTIER_CAP = 64;
+
+// Status codes (identical to include/crdt_gpu.h and the oracle)
+enum : i32 {
+  ST_OK = 0,
+  ST_POS_OOB = -1,
+  ST_SEQ = -2,
+  ST_UNKNOWN_AGENT = -3,
+  ST_UNKNOWN_ID = -4,
+  ST_NONTERMINATING = -5,
+  ST_CAPACITY = -6,
+  ST_EMPTY_TXN = -7,
+  ST_FRONTIER = -8,
+  ST_BAD_INPUT = -9,
+  ST_INTERNAL = -10,
+  ST_NEED_CAPACITY = -11,  // resumable: the txn at rec_pos was not started; grow (cap_need) and relaunch
+};
+
+struct Span {  // YjsSpan, 16 B
+  u32 order, ol, orr;
+  i32 len;
+};
+
+CRDT_HD u32 slen(const Span& s) { return (u32)(s.len < 0 ? -s.len : s.len); }
+CRDT_HD u32 clen(const Span& s) { return s.len > 0 ? (u32)s.len : 0u; }
+CRDT_HD i32 sgn(i32 x) { return (x > 0) - (x < 0); }
+CRDT_HD u32 origin_left_at_offset(const Span& s, u32 at) { return at == 0 ? s.ol : s.order + at - 1; }
+CRDT_HD Span truncate(Span& s, u32 at) {  // span.rs:33-45
+  i32 at_s = (i32)at * sgn(s.len);
+  Span o{s.order + at, s.order + at - 1, s.orr, s.len - at_s};
+  s.len = at_s;
+  return o;
+}
+CRDT_HD Span truncate_keeping_right(Span& s, u32 at) {  // span.rs:68-85
+  i32 at_s = (i32)at * sgn(s.len);
+  Span o{s.order, s.ol, s.orr, at_s};
+  s.order += at;
+  s.ol = s.order - 1;
+  s.len -= at_s;
+  return o;
+}
+CRDT_HD bool can_append(const Span& a, const Span& b) {  // span.rs:47-53
+  return ((a.len > 0) == (b.len > 0)) && b.order == a.order + slen(a) && b.ol == b.order - 1 && b.orr == a.orr;
+}
+
+struct CwoRun { u32 key, agent, seq, len; };   // client_with_order
+struct ARun { u32 key, order, len, pad; };     // item_orders of one agent (seq -> order)
+struct DelRun { u32 key, order, len; };        // deletes
+struct DDRun { u32 key, len, excess; };        // double_deletes
+struct TxnRec { u32 order, len, shadow, poff, pn, pad[3]; };  // txns (32 B)
+struct AgentRec { u32 run_base, run_cnt, run_cap, rank; };   // per-document agent table
+struct GroupRec { u32 blk, cnt, vis, pad; };   // persisted root level of the directory
+
+// ---------------------------------------------------------------------------------------------
+// Op record stream (16 B records, per document, in causal order)
+// ---------------------------------------------------------------------------------------------
+enum : u32 { REC_LTXN = 1, REC_LOP = 2, REC_RTXN = 3, REC_RINS = 4, REC_RDEL = 5, REC_RPARENT = 6 };
+struct Rec { u32 w0, w1, w2, w3; };
+// LTXN    w0 = kind<<28 | n_ops         w1 = agent                  w2 = sum(del) w3 = txn_len
+// LOP     w0 = kind<<28                 w1 = pos                    w2 = del   w3 = ins
+// RTXN    w0 = kind<<28 | zero_op<<27 | n_ops (27b)
+//                                       w1 = agent | n_parents<<16  w2 = seq   w3 = txn_len
+// RINS    w0 = kind<<28 | len (28b)     w1 = ol_agent | or_agent<<16  w2 = ol_seq  w3 = or_seq
+// RDEL    w0 = kind<<28 | len (28b)     w1 = agent                  w2 = seq
+// RPARENT w0 = kind<<28                 w1 = agent                  w2 = seq
+// (remote ops follow their RTXN, then the txn's RPARENT records)
+CRDT_HD u32 rec_kind(const Rec& r) { return r.w0 >> 28; }
+
+// ---------------------------------------------------------------------------------------------
+// Per-document segments (host-assigned, read-only during replay) and mutable header
+// ---------------------------------------------------------------------------------------------
+enum : u32 { DOC_TRACK_MAP = 1u };
+
+struct DocSeg {
+  u64 leaf_base;   // first leaf (pool index) of this doc; entries at leaf_base*L
+  u64 blk_base;    // first directory block; slots at blk_base*64
+  u64 map_base;    // order -> leaf table (u32 per order)
+  u64 cwo_base, arun_base, del_base, dd_base, txn_base, par_base, fr_base, agent_base, grp_base;
+  u64 rec_base;    // first record of this call's stream
+  u32 leaf_cap, blk_cap, map_cap, cwo_cap;
+  u32 arun_cap, del_cap, dd_cap, txn_cap;
+  u32 par_cap, agent_cap, rec_n, flags;
+};
+
+struct DocState {
+  i32 status;
+  u32 rec_pos;     // records of the current stream already applied (resume point)
+  u32 n_leaves, n_blocks;
+  u32 ng, next_order, len, n_cwo;
+  u32 n_del, n_dd, n_txn, n_par;
+  u32 n_fr, n_agents, n_items, cap_need;
+};
+
+struct Pools {
+  Span* leaves;        // [leaf][L]
+  u32* dir_leaf;       // [blk*64 + i]
+  u32* dir_vis;
+  u32* slot_of_leaf;   // [leaf_base + leaf] = blk<<6 | i
+  u32* leaf_of;        // [map_base + order]
+  CwoRun* cwo;
+  ARun* arun;
+  DelRun* dels;
+  DDRun* dd;
+  TxnRec* txns;
+  u32* parents;
+  u32* frontier;       // [fr_base .. + FRONTIER_CAP]
+  AgentRec* agents;
+  GroupRec* groups;    // [grp_base .. + MAX_GROUPS]
+  const Rec* recs;
+  const DocSeg* seg;
+  DocState* st;
+};
+
+}  // namespace crdt

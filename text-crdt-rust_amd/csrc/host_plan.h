@@ -1,0 +1,196 @@
+// Host-side planning for the replay kernel: agent interning (ListCRDT::get_or_create_agent_id,
+// doc.rs:66-89), encoding of local txns / remote wire batches into the device record stream,
+// and per-document capacity planning.  Used by the engine (engine.cpp) and by the test-only CPU
+// emulation harness (tests/emu).
+#pragma once
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "crdt_types.h"
+
+namespace crdt {
+
+// Remote wire batch (see include/crdt_gpu.h):  'RTX1', name table, txns.
+struct WireTxnView {
+  u32 agent_name, seq, n_parents, n_ops;
+  const u32* parents;  // pairs
+  const u32* ops;      // 6 words each
+};
+struct WireView {
+  std::vector<std::string> names;
+  std::vector<WireTxnView> txns;
+  bool parse(const uint8_t* p, size_t len) {
+    size_t off = 0;
+    auto rd = [&](u32& v) -> bool {
+      if (off + 4 > len) return false;
+      std::memcpy(&v, p + off, 4);
+      off += 4;
+      return true;
+    };
+    u32 magic, nn;
+    if (!rd(magic) || magic != 0x31585452u || !rd(nn)) return false;
+    names.resize(nn);
+    for (u32 i = 0; i < nn; i++) {
+      u32 bl;
+      if (!rd(bl) || off + bl > len) return false;
+      names[i].assign((const char*)p + off, bl);
+      off += (bl + 3) & ~3u;
+    }
+    u32 nt;
+    if (!rd(nt)) return false;
+    if (off % 4) return false;
+    txns.resize(nt);
+    for (u32 t = 0; t < nt; t++) {
+      WireTxnView& x = txns[t];
+      if (!rd(x.agent_name) || !rd(x.seq) || !rd(x.n_parents) || !rd(x.n_ops)) return false;
+      if (x.agent_name >= nn) return false;
+      if (off + 8ull * x.n_parents + 24ull * x.n_ops > len) return false;
+      x.parents = (const u32*)(p + off);
+      off += 8ull * x.n_parents;
+      x.ops = (const u32*)(p + off);
+      off += 24ull * x.n_ops;
+      for (u32 k = 0; k < x.n_parents; k++) if (x.parents[2 * k] >= nn) return false;
+      for (u32 k = 0; k < x.n_ops; k++) {
+        const u32* o = x.ops + 6 * k;
+        if (o[0] > 1 || o[1] >= nn || (o[0] == 0 && o[3] >= nn)) return false;
+      }
+    }
+    return true;
+  }
+};
+
+// Per-document host metadata: agent names (creation order) and name ranks.
+struct AgentTable {
+  std::vector<std::string> names;
+  std::unordered_map<std::string, u32> ids;
+  // ListCRDT::get_or_create_agent_id
+  u32 get_or_create(const std::string& n) {
+    if (n == "ROOT") return ROOT_AGENT;
+    auto it = ids.find(n);
+    if (it != ids.end()) return it->second;
+    u32 id = (u32)names.size();
+    names.push_back(n);
+    ids[n] = id;
+    return id;
+  }
+  // ListCRDT::get_agent_id (lookup only; unknown -> UNKNOWN_AGENT)
+  u32 lookup(const std::string& n) const {
+    if (n == "ROOT") return ROOT_AGENT;
+    auto it = ids.find(n);
+    return it == ids.end() ? UNKNOWN_AGENT : it->second;
+  }
+  // rank[a] = position of names[a] in byte-lexicographic order (Rust str Ord)
+  std::vector<u32> ranks() const {
+    std::vector<u32> idx(names.size());
+    for (u32 i = 0; i < idx.size(); i++) idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&](u32 a, u32 b) { return names[a] < names[b]; });
+    std::vector<u32> r(names.size());
+    for (u32 i = 0; i < idx.size(); i++) r[idx[i]] = i;
+    return r;
+  }
+};
+
+// Statistics of a record stream, for capacity planning.
+struct StreamNeeds {
+  u64 n_txn = 0, n_ltxn = 0, n_rtxn = 0, n_ops = 0, orders = 0, local_del = 0, remote_del_ops = 0, remote_parents = 0;
+  std::vector<u32> txns_per_agent;
+  void agent_txn(u32 a) {
+    if (a >= 0xFFFE) return;
+    if (txns_per_agent.size() <= a) txns_per_agent.resize(a + 1, 0);
+    txns_per_agent[a]++;
+  }
+};
+
+// Encode one local txn (LocalOp list, common.rs:45-50) for `agent`.
+inline void encode_local_txn(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, const u32* ops3, u32 nops) {
+  u64 span = 0, dels = 0;
+  for (u32 k = 0; k < nops; k++) { span += (u64)ops3[3 * k + 1] + ops3[3 * k + 2]; dels += ops3[3 * k + 1]; }
+  u32 span32 = span > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)span;
+  u32 dels32 = dels > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)dels;
+  out.push_back(Rec{(REC_LTXN << 28) | (nops & 0x0FFFFFFFu), agent, dels32, span32});
+  for (u32 k = 0; k < nops; k++) {
+    out.push_back(Rec{REC_LOP << 28, ops3[3 * k], ops3[3 * k + 1], ops3[3 * k + 2]});
+    nd.local_del += ops3[3 * k + 1];
+  }
+  nd.n_txn++;
+  nd.n_ltxn++;
+  nd.n_ops += nops;
+  nd.orders += span;
+  nd.agent_txn(agent);
+}
+
+// Encode a remote wire batch for one document, interning authors in txn order exactly as
+// apply_remote_txn does (doc.rs:243 get_or_create for the author; doc.rs:237 lookup for ids).
+inline void encode_remote(std::vector<Rec>& out, StreamNeeds& nd, AgentTable& at, const WireView& wv) {
+  std::vector<u32> cache(wv.names.size(), 0xFFFFFFFFu);
+  for (const WireTxnView& t : wv.txns) {
+    size_t before = at.names.size();
+    u32 author = at.get_or_create(wv.names[t.agent_name]);
+    if (at.names.size() != before)  // a new agent exists from now on: forget negative lookups
+      for (u32 i = 0; i < cache.size(); i++) if (cache[i] == UNKNOWN_AGENT) cache[i] = 0xFFFFFFFFu;
+    auto res = [&](u32 ni) -> u32 {
+      if (cache[ni] == 0xFFFFFFFFu) cache[ni] = at.lookup(wv.names[ni]);
+      return cache[ni];
+    };
+    u64 tl = 0;
+    bool zero = false;
+    for (u32 k = 0; k < t.n_ops; k++) {
+      u32 len = t.ops[6 * k + 5];
+      if (len == 0 || len > 0x0FFFFFFFu) zero = true;
+      tl += len;
+    }
+    u32 tl32 = tl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)tl;
+    out.push_back(Rec{(REC_RTXN << 28) | ((zero ? 1u : 0u) << 27) | (t.n_ops & 0x07FFFFFFu),
+                      (author & 0xFFFFu) | ((t.n_parents & 0xFFFFu) << 16), t.seq, tl32});
+    for (u32 k = 0; k < t.n_ops; k++) {
+      const u32* o = t.ops + 6 * k;
+      u32 len = o[5] & 0x0FFFFFFFu;
+      if (o[0] == 0) {
+        out.push_back(Rec{(REC_RINS << 28) | len, (res(o[1]) & 0xFFFFu) | ((res(o[3]) & 0xFFFFu) << 16), o[2], o[4]});
+      } else {
+        out.push_back(Rec{(REC_RDEL << 28) | len, res(o[1]) & 0xFFFFu, o[2], 0});
+        nd.remote_del_ops++;
+      }
+    }
+    for (u32 k = 0; k < t.n_parents; k++)
+      out.push_back(Rec{REC_RPARENT << 28, res(t.parents[2 * k]) & 0xFFFFu, t.parents[2 * k + 1], 0});
+    nd.n_txn++;
+    nd.n_rtxn++;
+    nd.n_ops += t.n_ops;
+    nd.orders += tl;
+    nd.remote_parents += t.n_parents;
+    nd.agent_txn(author);
+  }
+}
+
+// Capacities for a fresh document that will apply `nd` (heuristic leaf capacity; everything
+// else is an upper bound).  Growth for leaves/blocks is handled by the caller on ST_CAPACITY.
+constexpr u32 MAX_LEAVES = 32 * (MAX_GROUPS - 1);  // root level holds <= MAX_GROUPS blocks
+
+struct Caps {
+  u32 leaf, blk, map, cwo, arun, del, dd, txn, par, agent;
+};
+inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_div = 48) {
+  Caps c;
+  u64 leaves = 64 + nd.n_ops / leaf_div;
+  c.leaf = (u32)std::min<u64>(leaves, 1 + 2 * nd.n_ops + 1);
+  if (c.leaf < 64) c.leaf = 64;
+  if (c.leaf > MAX_LEAVES) c.leaf = MAX_LEAVES;
+  c.blk = c.leaf / 32 + 2;
+  c.map = track ? (u32)std::min<u64>(nd.orders + 1, 0xFFFFFFFFull) : 0;
+  c.cwo = (u32)nd.n_txn + 1;
+  c.txn = (u32)nd.n_txn + 1;
+  u64 arun = 0;
+  for (u32 a = 0; a < n_agents; a++) arun += (a < nd.txns_per_agent.size() ? nd.txns_per_agent[a] : 0) + 1;
+  c.arun = (u32)arun;
+  c.del = (u32)std::min<u64>(nd.local_del + nd.remote_del_ops + 1, 0xFFFFFFFFull);
+  c.dd = (u32)std::min<u64>(4 * nd.remote_del_ops + 64, 1u << 24);
+  c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + FRONTIER_CAP + 1, 0xFFFFFFFFull);
+  c.agent = n_agents;
+  return c;
+}
+
+}  // namespace crdt

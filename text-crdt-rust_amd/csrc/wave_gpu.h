@@ -1,0 +1,315 @@
+// WaveGPU: the CDNA4 (gfx950, wave64) backend of replay_core.h.
+//
+// One wavefront owns one document.  Lane-parallel state held in VGPRs:
+//   * the leaf cache: lane i < L holds entry i of the cached leaf (4 VGPRs: order, ol, orr, len);
+//   * the directory root: lane g of register r holds group 64r+g (block id, slot count, visible
+//     count), up to 4 registers = 256 groups = 16384 leaves per document.
+// Cross-lane steps use DPP row_shr / row_bcast scans (GFX9 form) and ds_bpermute shuffles;
+// uniform values are pulled to SGPRs with readfirstlane / readlane.
+#pragma once
+#include "crdt_types.h"
+
+namespace crdt {
+
+__device__ __forceinline__ u32 lane_id() { return __lane_id(); }
+__device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ u32 rdlane(u32 x, u32 l) { return __builtin_amdgcn_readlane(x, l); }
+__device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ u32 shfl(u32 v, u32 src) { return __builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
+
+// Inclusive wave64 prefix sum (LLVM AMDGPUAtomicOptimizer GFX9 sequence).
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return v;
+}
+__device__ __forceinline__ u32 wave_sum(u32 v) { return rdlane(wave_incl_scan(v), 63); }
+
+struct Slots4 {  // 4 VGPRs indexed by a wave-uniform register number
+  u32 r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  __device__ __forceinline__ u32 get(u32 r) const { return r == 0 ? r0 : r == 1 ? r1 : r == 2 ? r2 : r3; }
+  __device__ __forceinline__ void put(u32 r, u32 v) {
+    if (r == 0) r0 = v; else if (r == 1) r1 = v; else if (r == 2) r2 = v; else r3 = v;
+  }
+};
+
+template <int L>
+struct WaveGPU {
+  // ---------------------------------------------------------------- leaf cache
+  u32 eo = 0, el = 0, er = 0;
+  i32 en = 0;
+  // ---------------------------------------------------------------- root level
+  Slots4 gb, gc, gv;
+
+  // ---- scalar memory helpers (every lane touches the same address: uniform results, and a
+  //      store is then visible to every lane's later loads by per-thread program order)
+  __device__ __forceinline__ u32 ld(const u32* p) const { return uni(*(volatile const u32*)p); }
+  __device__ __forceinline__ void st(u32* p, u32 v) const { *(volatile u32*)p = v; }
+  __device__ __forceinline__ void st(i32* p, i32 v) const { *(volatile i32*)p = v; }
+  template <class T> __device__ __forceinline__ T ldT(const T* p) const {
+    T t;
+    const volatile u32* s = (const volatile u32*)p;
+    u32* o = (u32*)&t;
+#pragma unroll
+    for (u32 k = 0; k < sizeof(T) / 4; k++) o[k] = uni(s[k]);
+    return t;
+  }
+  template <class T> __device__ __forceinline__ void stT(T* p, const T& v) const {
+    volatile u32* s = (volatile u32*)p;
+    const u32* o = (const u32*)&v;
+#pragma unroll
+    for (u32 k = 0; k < sizeof(T) / 4; k++) s[k] = o[k];
+  }
+  __device__ __forceinline__ AgentRec ld_agent(const AgentRec* p) const { return ldT(p); }
+  __device__ __forceinline__ ARun ld_arun(const ARun* p) const { return ldT(p); }
+  __device__ __forceinline__ void st_arun(ARun* p, const ARun& v) const { stT(p, v); }
+  __device__ __forceinline__ CwoRun ld_cwo(const CwoRun* p) const { return ldT(p); }
+  __device__ __forceinline__ void st_cwo(CwoRun* p, const CwoRun& v) const { stT(p, v); }
+  __device__ __forceinline__ DelRun ld_del(const DelRun* p) const { return ldT(p); }
+  __device__ __forceinline__ void st_del(DelRun* p, const DelRun& v) const { stT(p, v); }
+  __device__ __forceinline__ DDRun ld_dd(const DDRun* p) const { return ldT(p); }
+  __device__ __forceinline__ void st_dd(DDRun* p, const DDRun& v) const { stT(p, v); }
+  __device__ __forceinline__ TxnRec ld_txn(const TxnRec* p) const { return ldT(p); }
+  __device__ __forceinline__ void st_txn(TxnRec* p, const TxnRec& v) const { stT(p, v); }
+  __device__ __forceinline__ Rec ld_rec(const Rec* p) const {
+    uint4 v = *(const uint4*)p;
+    return Rec{uni(v.x), uni(v.y), uni(v.z), uni(v.w)};
+  }
+  __device__ __forceinline__ void st_state(DocState* p, const DocState& s) const { stT(p, s); }
+
+  // lane-parallel fill of n u32
+  __device__ __forceinline__ void fill(u32* p, u32 n, u32 v) const {
+    for (u32 k = lane_id(); k < n; k += 64) p[k] = v;
+  }
+  __device__ __forceinline__ void zero_leaf(Span* p, u32 n) const {
+    u32 l = lane_id();
+    if (l < n) *(uint4*)(p + l) = make_uint4(0, 0, 0, 0);
+  }
+
+  // 64-ary search over sorted runs: index k with key(k) <= needle < key(k)+len(k), or -1.
+  template <class T>
+  __device__ __forceinline__ i32 search(const T* base, u32 n, u32 needle) const {
+    if (n == 0) return -1;
+    u32 lo = 0, hi = n;  // answer (last key <= needle) in [lo, hi)
+    u32 l = lane_id();
+    while (hi - lo > 64) {
+      u32 step = (hi - lo + 63) / 64;
+      u32 idx = lo + l * step;
+      bool ok = idx < hi && *(const volatile u32*)&base[idx] <= needle;  // key is the first field
+      u64 m = ballot(ok);
+      if (m == 0) return -1;
+      u32 t = 63 - __builtin_clzll(m);
+      lo = lo + t * step;
+      u32 nh = lo + step;
+      hi = nh < hi ? nh : hi;
+    }
+    u32 idx = lo + l;
+    bool ok = idx < hi && *(const volatile u32*)&base[idx] <= needle;
+    u64 m = ballot(ok);
+    if (m == 0) return -1;
+    u32 k = lo + (63 - __builtin_clzll(m));
+    T r = ldT(base + k);
+    u32 key = ((const u32*)&r)[0];
+    u32 len = rlen(r);
+    return (needle < key + len) ? (i32)k : -1;
+  }
+  __device__ __forceinline__ static u32 rlen(const ARun& r) { return r.len; }
+  __device__ __forceinline__ static u32 rlen(const CwoRun& r) { return r.len; }
+  __device__ __forceinline__ static u32 rlen(const DDRun& r) { return r.len; }
+  __device__ __forceinline__ static u32 rlen(const TxnRec& r) { return r.len; }
+  __device__ __forceinline__ i32 search_arun(const ARun* b, u32 n, u32 x) const { return search(b, n, x); }
+  __device__ __forceinline__ i32 search_cwo(const CwoRun* b, u32 n, u32 x) const { return search(b, n, x); }
+  __device__ __forceinline__ i32 search_dd(const DDRun* b, u32 n, u32 x) const { return search(b, n, x); }
+  __device__ __forceinline__ i32 search_txn(const TxnRec* b, u32 n, u32 x) const { return search(b, n, x); }
+
+  // ---------------------------------------------------------------- leaf cache
+  __device__ __forceinline__ u32 cache_load(const Span* p) {
+    u32 l = lane_id();
+    if (l < (u32)L) {
+      uint4 v = *(const volatile uint4*)(p + l);
+      eo = v.x; el = v.y; er = v.z; en = (i32)v.w;
+    } else { eo = el = er = 0; en = 0; }
+    return __popcll(ballot(l < (u32)L && en != 0));
+  }
+  __device__ __forceinline__ void cache_store(Span* p, u32 /*n*/) const {
+    u32 l = lane_id();
+    if (l < (u32)L) *(volatile uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
+  }
+  __device__ __forceinline__ Span cget(u32 i) const {
+    return Span{rdlane(eo, i), rdlane(el, i), rdlane(er, i), (i32)rdlane((u32)en, i)};
+  }
+  __device__ __forceinline__ void cset(u32 i, const Span& s) {
+    if (lane_id() == i) { eo = s.order; el = s.ol; er = s.orr; en = s.len; }
+  }
+  __device__ __forceinline__ u32 clen_l() const { return en > 0 ? (u32)en : 0u; }
+  __device__ __forceinline__ u32 cache_vis(u32 a, u32 b) const {
+    u32 l = lane_id();
+    return wave_sum((l >= a && l < b) ? clen_l() : 0u);
+  }
+  // leaf.rs:61-84 find_offset (stick_end = false) over clen
+  __device__ __forceinline__ bool cfind_content(u32 n, u32 rem, u32& idx, u32& off) const {
+    u32 l = lane_id();
+    u32 x = l < n ? clen_l() : 0u;
+    u32 incl = wave_incl_scan(x);
+    u32 k = __popcll(ballot(l < n && incl <= rem));
+    if (k < n) {
+      idx = k;
+      off = rem - (rdlane(incl, k) - rdlane(x, k));
+      return true;
+    }
+    u32 total = n ? rdlane(incl, n - 1) : 0u;
+    if (rem == total) { idx = n; off = 0; return true; }
+    return false;
+  }
+  // leaf.rs:41-57 find
+  __device__ __forceinline__ i32 cfind_order(u32 n, u32 order) const {
+    u32 l = lane_id();
+    u32 sl = (u32)(en < 0 ? -en : en);
+    u64 m = ballot(l < n && order >= eo && order - eo < sl);
+    return m ? (i32)(__builtin_ctzll(m)) : -1;
+  }
+  __device__ __forceinline__ void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) const {
+    u32 l = lane_id();
+    u32 src = l + idx - padding;  // valid only when l >= padding
+    u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
+    bool take = l >= padding && src < n;
+    if (l < (u32)L) *(volatile uint4*)(dst + l) = take ? make_uint4(o, a, b, c) : make_uint4(0, 0, 0, 0);
+  }
+  __device__ __forceinline__ void cache_clear(u32 a, u32 b) {
+    u32 l = lane_id();
+    if (l >= a && l < b) { eo = el = er = 0; en = 0; }
+  }
+  __device__ __forceinline__ void cache_shift_right(u32 idx, u32 n, u32 k) {
+    u32 l = lane_id();
+    u32 src = l - k;
+    u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
+    if (l >= idx + k && l < n + k) { eo = o; el = a; er = b; en = (i32)c; }
+  }
+
+  // ---------------------------------------------------------------- directory root (VGPRs)
+  __device__ __forceinline__ void root_init(u32 blk, u32 cnt, u32 vis) {
+    gb = Slots4(); gc = Slots4(); gv = Slots4();
+    if (lane_id() == 0) { gb.r0 = blk; gc.r0 = cnt; gv.r0 = vis; }
+  }
+  __device__ __forceinline__ void root_load(const GroupRec* g, u32 ng) {
+    u32 l = lane_id();
+#pragma unroll
+    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
+      u32 i = r * 64 + l;
+      u32 b = 0, c = 0, v = 0;
+      if (i < ng) { uint4 x = *(const volatile uint4*)(g + i); b = x.x; c = x.y; v = x.z; }
+      gb.put(r, b); gc.put(r, c); gv.put(r, v);
+    }
+  }
+  __device__ __forceinline__ void root_store(GroupRec* g, u32 ng) const {
+    u32 l = lane_id();
+#pragma unroll
+    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
+      u32 i = r * 64 + l;
+      if (i < ng) *(volatile uint4*)(g + i) = make_uint4(gb.get(r), gc.get(r), gv.get(r), 0);
+    }
+  }
+  __device__ __forceinline__ u32 root_blk(u32 g) const { return rdlane(gb.get(g >> 6), g & 63); }
+  __device__ __forceinline__ u32 root_cnt(u32 g) const { return rdlane(gc.get(g >> 6), g & 63); }
+  __device__ __forceinline__ u32 root_vis(u32 g) const { return rdlane(gv.get(g >> 6), g & 63); }
+  __device__ __forceinline__ u32 root_find_blk(u32 ng, u32 blk) const {
+    u32 l = lane_id();
+#pragma unroll
+    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
+      if (r * 64 >= ng) break;
+      u64 m = ballot(r * 64 + l < ng && gb.get(r) == blk);
+      if (m) return r * 64 + __builtin_ctzll(m);
+    }
+    return INVALID;
+  }
+  __device__ __forceinline__ void root_add_vis(u32 g, u32 delta) {
+    u32 r = g >> 6;
+    if (lane_id() == (g & 63)) gv.put(r, gv.get(r) + delta);
+  }
+  __device__ __forceinline__ void root_set(u32 g, u32 blk, u32 cnt, u32 vis) {
+    u32 r = g >> 6;
+    if (lane_id() == (g & 63)) { gb.put(r, blk); gc.put(r, cnt); gv.put(r, vis); }
+  }
+  // insert a group at index g, shifting [g, ng) up by one
+  __device__ __forceinline__ void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
+    u32 l = lane_id();
+    Slots4 nb = gb, nc = gc, nv = gv;
+#pragma unroll
+    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
+      if (r * 64 > ng) break;
+      u32 pb = r ? rdlane(gb.get(r - 1), 63) : 0u;
+      u32 pc = r ? rdlane(gc.get(r - 1), 63) : 0u;
+      u32 pv = r ? rdlane(gv.get(r - 1), 63) : 0u;
+      u32 sb = shfl(gb.get(r), l - 1), sc = shfl(gc.get(r), l - 1), sv = shfl(gv.get(r), l - 1);
+      if (l == 0) { sb = pb; sc = pc; sv = pv; }
+      u32 i = r * 64 + l;
+      if (i > g && i <= ng) { nb.put(r, sb); nc.put(r, sc); nv.put(r, sv); }
+    }
+    gb = nb; gc = nc; gv = nv;
+    root_set(g, blk, cnt, vis);
+  }
+  // first group whose cumulative visible count exceeds pos
+  __device__ __forceinline__ bool root_find_pos(u32 ng, u32 pos, u32& g, u32& base) const {
+    u32 l = lane_id();
+    u32 carry = 0;
+#pragma unroll
+    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
+      if (r * 64 >= ng) break;
+      bool valid = r * 64 + l < ng;
+      u32 x = valid ? gv.get(r) : 0u;
+      u32 incl = wave_incl_scan(x) + carry;
+      u32 nvalid = ng - r * 64 < 64 ? ng - r * 64 : 64;
+      u32 k = __popcll(ballot(valid && incl <= pos));
+      if (k < nvalid) {
+        g = r * 64 + k;
+        base = rdlane(incl, k) - rdlane(x, k);
+        return true;
+      }
+      carry = rdlane(incl, 63);
+    }
+    return false;
+  }
+
+  // ---------------------------------------------------------------- directory blocks (HBM)
+  __device__ __forceinline__ bool blk_find_pos(const u32* dv, u32 cnt, u32 rem, u32& i, u32& before) const {
+    u32 l = lane_id();
+    u32 x = l < cnt ? *(const volatile u32*)(dv + l) : 0u;
+    u32 incl = wave_incl_scan(x);
+    u32 k = __popcll(ballot(l < cnt && incl <= rem));
+    if (k >= cnt) return false;
+    i = k;
+    before = rdlane(incl, k) - rdlane(x, k);
+    return true;
+  }
+  __device__ __forceinline__ void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+    u32 l = lane_id();
+    u32 ol = l < cnt ? *(volatile u32*)(dl + l) : 0u;
+    u32 ov = l < cnt ? *(volatile u32*)(dv + l) : 0u;
+    u32 sl = shfl(ol, l - 1), sv = shfl(ov, l - 1);
+    u32 nlf = l < i ? ol : (l == i ? leaf : sl);
+    u32 nvs = l < i ? ov : (l == i ? vis : sv);
+    if (l >= i && l <= cnt) {
+      *(volatile u32*)(dl + l) = nlf;
+      *(volatile u32*)(dv + l) = nvs;
+      *(volatile u32*)(sol + nlf) = (blk << 6) | l;
+    }
+  }
+  __device__ __forceinline__ u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
+    u32 l = lane_id();
+    u32 lf = 0, v = 0;
+    if (l >= 32) {
+      lf = *(const volatile u32*)(dl + l);
+      v = *(const volatile u32*)(dv + l);
+      *(volatile u32*)(ndl + l - 32) = lf;
+      *(volatile u32*)(ndv + l - 32) = v;
+      *(volatile u32*)(sol + lf) = (nb << 6) | (l - 32);
+    }
+    return wave_sum(v);
+  }
+};
+
+}  // namespace crdt
