@@ -1,0 +1,155 @@
+/*
+ * crdt_gpu.h — C ABI of the MI355X list-CRDT engine (drop-in boundary for the hot path of
+ * josephg/text-crdt-rust: position <-> CRDT-location remapping and batch merge of list-CRDT
+ * edits, across many documents at once).
+ *
+ * The reference exposes this path only as a Rust crate API (src/lib.rs:3-14); there is no FFI.
+ * Each entry point below names the reference function it replaces; a Rust binding would wrap
+ * these in `ListCRDT`-shaped methods (see INTEGRATION.md for the cgo-free Rust `extern "C"`
+ * block and a ctypes stub).
+ *
+ * Conventions
+ *   - Caller-owned host buffers; the engine owns device memory.  Calls are synchronous at return
+ *     unless named *_async (then crdt_sync()).  One engine per host thread per device.
+ *   - Positions and lengths count Unicode scalar values (chars().count(), doc.rs:383).
+ *   - Agent 0xFFFF = ROOT (doc.rs:68).  Order 0xFFFFFFFF = ROOT_ORDER (list/mod.rs:30).
+ *   - A failing op poisons only its document (doc_status < 0); later ops of that document are
+ *     skipped.  This mirrors "the reference panics": the document is dead, the rest live on.
+ *   - Return value of every function: 0 = ok, < 0 = API error (CRDT_E_*).
+ */
+#ifndef CRDT_GPU_H
+#define CRDT_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- per-document status codes (identical in the oracle and the kernels) ---------------- */
+#define CRDT_OK 0
+#define CRDT_ERR_POS_OOB -1          /* local op outside the document (root.rs:71,79; mutations.rs:573) */
+#define CRDT_ERR_SEQ -2              /* remote txn seq != next seq of its agent (doc.rs:247) */
+#define CRDT_ERR_UNKNOWN_AGENT -3    /* agent name/id not known to the document (doc.rs:92,237) */
+#define CRDT_ERR_UNKNOWN_ID -4       /* (agent, seq) does not name an inserted item (doc.rs:27, root.rs:288) */
+#define CRDT_ERR_NONTERMINATING -5   /* the reference's integrate / remote-delete loop never exits here */
+#define CRDT_ERR_CAPACITY -6         /* a per-document structural limit was exceeded */
+#define CRDT_ERR_EMPTY_TXN -7        /* zero-length txn (reference underflows first_order+0-1, doc.rs:351) */
+#define CRDT_ERR_FRONTIER -8         /* advance_branch_by assertion (doc.rs:43) */
+#define CRDT_ERR_BAD_INPUT -9        /* malformed record / zero-length remote op */
+#define CRDT_ERR_INTERNAL -10
+
+/* ---- API errors ---------------------------------------------------------------------------- */
+#define CRDT_E_ARG -100
+#define CRDT_E_DEVICE -101   /* no usable MI355X / HIP error */
+#define CRDT_E_NOMEM -102
+#define CRDT_E_WIRE -103     /* malformed remote wire batch */
+
+typedef struct crdt_engine crdt_engine;
+
+typedef struct {
+  uint32_t leaf_cap;   /* 32 = reference release layout (range_tree/mod.rs:38), 4 = debug layout */
+  int32_t device;      /* HIP device ordinal */
+} crdt_cfg;
+
+/* LocalOp (src/common.rs:45-50) with the inserted string replaced by its char count. */
+typedef struct {
+  uint32_t pos;
+  uint32_t del_len;
+  uint32_t ins_len;
+} crdt_local_op;
+
+/* One apply_local_txn(agent, &ops[..n_ops]) call (doc.rs:376). */
+typedef struct {
+  uint32_t agent;
+  uint32_t n_ops;
+} crdt_local_txn;
+
+/* ListCRDT::new() x n — (re)creates n_docs empty documents (doc.rs:51-64). */
+int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out);
+void crdt_engine_destroy(crdt_engine* e);
+int crdt_docs_alloc(crdt_engine* e, uint64_t n_docs);
+uint64_t crdt_num_docs(const crdt_engine* e);
+
+/* ListCRDT::get_or_create_agent_id (doc.rs:66-80), n independent (doc, name) requests. */
+int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const char* const* names,
+                      uint16_t* agent_out);
+
+/* ListCRDT::apply_local_txn (doc.rs:376-469) for many documents.  Document docs[i] applies txns
+ * txns[txn_off[i] .. txn_off[i+1]) in order; ops are concatenated in txn order. */
+int crdt_apply_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
+                     const crdt_local_txn* txns, const crdt_local_op* ops, int32_t* doc_status);
+
+/* ListCRDT::apply_remote_txn (doc.rs:242-348) for many documents: wire[i] (wire_len[i] bytes) is
+ * a remote wire batch applied to docs[i].
+ *
+ * Remote wire batch (serialises RemoteTxn, src/list/external_txn.rs:5-30; little endian u32s):
+ *   'RTX1' (0x31585452) | n_names | n_names x {byte_len, utf-8 bytes, zero pad to 4}
+ *   | n_txns | n_txns x { agent_name, seq, n_parents, n_ops,
+ *                         n_parents x {name, seq},
+ *                         n_ops x {kind (0 Ins, 1 Del), a_name, a_seq, b_name, b_seq, len} }
+ *   Ins: a = origin_left, b = origin_right, len = chars inserted.  Del: a = target, len.
+ *   The name "ROOT" denotes the root id (doc.rs:68). */
+int crdt_apply_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs,
+                           const uint8_t* const* wire, const uint64_t* wire_len, int32_t* doc_status);
+
+/* Staged form (inputs resident in HBM, then replay without host transfers): */
+int crdt_stage_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
+                     const crdt_local_txn* txns, const crdt_local_op* ops);
+int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs,
+                           const uint8_t* const* wire, const uint64_t* wire_len);
+/* One wire batch replicated to docs [0, n_docs) of a fresh engine; name index `rename_idx` of the
+ * batch's name table is replaced per document by names[d] (randomised client ids). */
+int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t wire_len,
+                                 uint32_t rename_idx, const char* const* names);
+/* Reset every document to ListCRDT::new() state, keeping interned agents and staged records. */
+int crdt_reset_async(crdt_engine* e);
+/* Replay the staged records of every document (+ capacity growth/resume as needed). */
+int crdt_run(crdt_engine* e, int32_t* doc_status /* n_docs, may be NULL */);
+int crdt_run_async(crdt_engine* e);   /* single launch; no growth handling */
+/* Rebuild the flat per-document index: canonical span array (stream compaction of the leaf
+ * entries with YjsSpan::can_append), visible-prefix scan, order->span scatter, digests. */
+int crdt_publish_async(crdt_engine* e);
+int crdt_sync(crdt_engine* e);
+
+/* ---- queries (the reference's README operations, README.md:22-25) ------------------------- */
+/* Doc location -> CRDT location (§3.3: cursor_at_content_pos + client_with_order.get).
+ * Invalid positions give agent 0xFFFF, seq 0xFFFFFFFF. */
+int crdt_pos_to_loc(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint32_t* pos,
+                    uint16_t* agent, uint32_t* seq);
+/* CRDT location -> doc location (§3.4: seq_to_order + Cursor::count_pos).  deleted: 0/1, 2 = unknown id. */
+int crdt_loc_to_pos(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint16_t* agent,
+                    const uint32_t* seq, uint32_t* pos, uint8_t* deleted);
+/* Device-pointer forms for batched query benchmarking (inputs/outputs already in HBM). */
+int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint32_t* pos,
+                              uint16_t* agent, uint32_t* seq);
+int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint16_t* agent,
+                              const uint32_t* seq, uint32_t* pos, uint8_t* deleted);
+
+/* ListCRDT::len (doc.rs:484-486) */
+int crdt_doc_len(crdt_engine* e, uint64_t n, const uint32_t* doc, uint32_t* len);
+int crdt_doc_status(crdt_engine* e, int32_t* status /* n_docs */);
+/* 64-bit digest of each document's canonical state (DESIGN.md "Digest"; same as the oracle). */
+int crdt_digest(crdt_engine* e, uint64_t* per_doc /* n_docs */);
+
+/* Export one document (parity / debugging).  sizes[12] = {raw entries, leaves, canonical spans,
+ * cwo runs, delete runs, double-delete runs, txns, parents, frontier, agents, next_order, len}.
+ * Any output pointer may be NULL.  raw/canon: 4 u32 per span (order, origin_left, origin_right,
+ * len as i32); cwo: (order, agent, seq, len); deletes/dd: 3 u32; txns: (order, len, shadow,
+ * parents_off, n_parents). */
+int crdt_export_sizes(crdt_engine* e, uint32_t doc, uint64_t* sizes);
+int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_sizes, uint32_t* canon4,
+                uint32_t* cwo4, uint32_t* del3, uint32_t* dd3, uint32_t* txn5, uint32_t* parents,
+                uint32_t* frontier);
+
+/* Device time of the last replay / publish launches in ms (HIP events on the engine stream). */
+int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms);
+/* Engine stream (hipStream_t) for callers that time or order their own work. */
+void* crdt_stream(crdt_engine* e);
+/* Text of the last HIP error seen by this thread (empty if none). */
+const char* crdt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRDT_GPU_H */

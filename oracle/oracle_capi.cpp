@@ -284,36 +284,40 @@ double orc_cpu_baseline_local(uint32_t ndocs, uint32_t threads, uint32_t ntxn, c
   return t1 - t0;
 }
 
-// Remote replay of a wire batch for `ndocs` documents; document i's agent names are the wire's
-// names with name index `rename_idx` replaced by names[i] (NUL-separated list).
+// Remote replay of a wire batch for `ndocs` documents (the reference takes &RemoteTxn, so each
+// worker materialises the RemoteTxn list once, before the timed region, with document i's name at
+// index `rename_idx` replaced by names[i] for the first document it owns; names never change the
+// amount of work of a single-agent trace).  Timed region: from a start barrier to the last join.
 double orc_cpu_baseline_remote(uint32_t ndocs, uint32_t threads, const uint8_t* buf, size_t len,
                                uint32_t rename_idx, const char* const* names, uint64_t* checksum) {
   wire::Batch b;
   if (!wire::parse(buf, len, b)) return -1.0;
-  // Materialise each document's RemoteTxn list up front (the reference takes &RemoteTxn).
-  std::vector<std::vector<RemoteTxn>> per_doc(ndocs);
-  for (uint32_t i = 0; i < ndocs; i++) {
-    wire::Batch bi = b;
-    if (rename_idx < bi.names.size()) bi.names[rename_idx] = names[i];
-    per_doc[i].reserve(bi.txns.size());
-    for (const auto& t : bi.txns) per_doc[i].push_back(bi.to_remote(t));
-  }
-  std::atomic<uint32_t> next{0};
+  std::atomic<uint32_t> next{0}, ready{0};
+  std::atomic<bool> go{false};
   std::atomic<uint64_t> sum{0};
-  auto worker = [&]() {
+  auto worker = [&](uint32_t tid) {
+    wire::Batch bi = b;
+    if (rename_idx < bi.names.size() && names) bi.names[rename_idx] = names[tid % ndocs];
+    std::vector<RemoteTxn> txns;
+    txns.reserve(bi.txns.size());
+    for (const auto& t : bi.txns) txns.push_back(bi.to_remote(t));
+    ready++;
+    while (!go.load()) std::this_thread::yield();
     uint64_t local = 0;
     while (true) {
       uint32_t i = next.fetch_add(1);
       if (i >= ndocs) break;
       Doc d(32, 16, true);
-      for (const auto& t : per_doc[i]) d.apply_remote_txn(t);
+      for (const auto& t : txns) d.apply_remote_txn(t);
       local += d.len() + (uint64_t)d.status;
     }
     sum += local;
   };
-  double t0 = now_s();
   std::vector<std::thread> ts;
-  for (uint32_t k = 0; k < threads; k++) ts.emplace_back(worker);
+  for (uint32_t k = 0; k < threads; k++) ts.emplace_back(worker, k);
+  while (ready.load() < threads) std::this_thread::yield();
+  double t0 = now_s();
+  go = true;
   for (auto& t : ts) t.join();
   double t1 = now_s();
   if (checksum) *checksum = sum.load();

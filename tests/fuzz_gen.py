@@ -1,0 +1,161 @@
+"""Seeded workload generators shared by CPU (emulator) and GPU parity tests — TEST INFRASTRUCTURE.
+
+random_local_trace: the reference's make_random_change (doc.rs:544-569): insert weight 0.55 if
+len < 100 else 0.45; insert 1 char at U[0, len]; delete U[1, min(10, len-pos)] at U[0, len-1].
+concurrent_wire: several agents editing their own replicas (oracle) and exchanging remote txns;
+returns one causally ordered wire batch that replays the whole history.
+"""
+import random
+import struct
+
+import numpy as np
+
+
+def random_local_trace(seed: int, n_ops: int, ins_max: int = 1):
+    rng = random.Random(seed)
+    n = 0
+    patches = []
+    for _ in range(n_ops):
+        w = 0.55 if n < 100 else 0.45
+        if n == 0 or rng.random() < w:
+            pos = rng.randint(0, n)
+            k = rng.randint(1, ins_max)
+            patches.append((pos, 0, k))
+            n += k
+        else:
+            pos = rng.randint(0, n - 1)
+            span = rng.randint(1, min(10, n - pos))
+            patches.append((pos, span, 0))
+            n -= span
+    p = np.array(patches, dtype=np.uint32).reshape(-1, 3)
+    return np.ones(p.shape[0], np.uint32), p
+
+
+def parse_wire(w: bytes):
+    """wire -> (names, txns[(agent, seq, parents[(name,seq)], ops[(kind,a,as,b,bs,len)])])."""
+    off = 0
+
+    def rd():
+        nonlocal off
+        v = struct.unpack_from("<I", w, off)[0]
+        off += 4
+        return v
+    assert rd() == 0x31585452
+    names = []
+    for _ in range(rd()):
+        bl = rd()
+        names.append(w[off:off + bl].decode())
+        off += (bl + 3) & ~3
+    txns = []
+    for _ in range(rd()):
+        a, s, np_, no = rd(), rd(), rd(), rd()
+        ps = [(names[rd()], rd()) for _ in range(np_)]
+        ops = []
+        for _ in range(no):
+            k, an, asq, bn, bsq, ln = rd(), rd(), rd(), rd(), rd(), rd()
+            ops.append((k, names[an], asq, names[bn] if k == 0 else None, bsq, ln))
+        txns.append((names[a], s, ps, ops))
+    return names, txns
+
+
+def build_wire(txns):
+    names = []
+
+    def ni(n):
+        if n not in names:
+            names.append(n)
+        return names.index(n)
+    body = []
+    for agent, seq, parents, ops in txns:
+        body += [ni(agent), seq, len(parents), len(ops)]
+        for pn, ps in parents:
+            body += [ni(pn), ps]
+        for k, an, asq, bn, bsq, ln in ops:
+            body += [k, ni(an), asq, ni(bn) if k == 0 else 0, bsq if k == 0 else 0, ln]
+    out = struct.pack("<II", 0x31585452, len(names))
+    for n in names:
+        b = n.encode()
+        out += struct.pack("<I", len(b)) + b + b"\0" * ((4 - len(b) % 4) % 4)
+    return out + struct.pack("<I", len(txns)) + np.array(body, dtype=np.uint32).tobytes()
+
+
+def concurrent_wire(seed: int, n_agents: int = 3, rounds: int = 6, ops_per_round: int = 4, base_len: int = 20):
+    """Agents edit replicas concurrently each round, then everyone merges everything.
+
+    Uses the oracle's local->remote recorder per replica.  Returns (wire, n_txns).
+    """
+    from oracle_lib import OracleDoc, lib, _p
+    import ctypes as C
+    rng = random.Random(seed)
+    L = lib()
+    names = [f"agent{chr(97 + i)}{rng.randint(0, 9)}" for i in range(n_agents)]
+    history = []  # causally ordered txn list (parsed)
+
+    def record(doc, agent_id, ops):
+        c = np.array([len(ops)], np.uint32)
+        p = np.array(ops, np.uint32).reshape(-1, 3)
+        n = L.orc_local_trace_to_wire(doc.h, agent_id, 1, _p(c), _p(p), None, 0)
+        # the sizing call applied the txn; fetch the bytes by re-running on a twin is not possible,
+        # so record via a scratch buffer call instead (apply once):
+        raise RuntimeError("use record2")
+
+    def record2(doc, agent_id, ops):
+        c = np.array([len(ops)], np.uint32)
+        p = np.array(ops, np.uint32).reshape(-1, 3)
+        buf = C.create_string_buffer(1 << 20)
+        n = L.orc_local_trace_to_wire(doc.h, agent_id, 1, _p(c), _p(p), C.cast(buf, C.c_void_p), 1 << 20)
+        if n < 0:
+            return None
+        return parse_wire(buf.raw[:n])[1]
+
+    reps = []
+    seen = []
+    for i in range(n_agents):
+        d = OracleDoc()
+        reps.append(d)
+        seen.append(0)
+    # base document by agent 0, delivered to everyone
+    a0 = reps[0].agent(names[0])
+    tx = record2(reps[0], a0, [(0, 0, base_len)])
+    history += tx
+    seen[0] = len(history)
+    for r in range(rounds):
+        # deliver everything not yet seen
+        for i in range(n_agents):
+            new = history[seen[i]:]
+            if new and i != 0 or (new and seen[i] < len(history)):
+                if reps[i].apply_remote_wire(build_wire(new)) != 0:
+                    return build_wire(history), len(history)
+            seen[i] = len(history)
+        snapshot = len(history)
+        round_txns = []
+        for i in range(n_agents):
+            ai = reps[i].agent(names[i])
+            for _ in range(ops_per_round):
+                n = len(reps[i])
+                if n == 0 or rng.random() < 0.6:
+                    op = (rng.randint(0, n), 0, rng.randint(1, 3))
+                else:
+                    pos = rng.randint(0, n - 1)
+                    op = (pos, rng.randint(1, min(4, n - pos)), 0)
+                t = record2(reps[i], ai, [op])
+                if t is None:
+                    break
+                round_txns.append((i, t))
+        # deliver in a shuffled but per-agent-ordered interleaving
+        order = list(range(len(round_txns)))
+        per = {}
+        for k, (i, t) in enumerate(round_txns):
+            per.setdefault(i, []).append(t)
+        seq = []
+        while any(per.values()):
+            i = rng.choice([k for k, v in per.items() if v])
+            seq += per[i].pop(0)
+        history += seq
+        for i in range(n_agents):
+            # each agent already has its own txns; mark them seen via full re-delivery of others
+            others = [t for t in history[snapshot:] if t[0] != names[i]]
+            if others and reps[i].apply_remote_wire(build_wire(others)) != 0:
+                return build_wire(history), len(history)
+            seen[i] = len(history)
+    return build_wire(history), len(history)

@@ -1,0 +1,166 @@
+"""GPU parity: the HIP engine (through the C ABI) against the oracle, bit-exact.
+
+Compared per document: raw entry layout + leaf boundaries (the reference's release B-tree leaves),
+canonical spans, client_with_order, deletes, double deletes, txns + parents, frontier, len,
+the 64-bit digest, and every pos->loc / loc->pos answer.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import crdt_amd  # noqa: E402
+from crdt_amd.traces import load_remote_wire, load_trace  # noqa: E402
+from oracle_lib import OracleDoc  # noqa: E402
+from fuzz_gen import random_local_trace  # noqa: E402
+
+KEYS = ("raw", "leaf_sizes", "canon", "cwo", "deletes", "dd", "txns", "parents", "frontier", "len", "next_order")
+
+
+def assert_same(g, o, keys=KEYS):
+    for k in keys:
+        x, y = g[k], o[k]
+        if isinstance(x, np.ndarray):
+            assert x.shape == y.shape, (k, x.shape, y.shape)
+            if not np.array_equal(x, y):
+                i = int(np.argwhere(x != y)[0][0])
+                raise AssertionError(f"{k} differs at {i}: gpu {x[i]} oracle {y[i]}")
+        else:
+            assert x == y, (k, x, y)
+
+
+def check_queries(e, doc, o):
+    n = len(o)
+    pos = np.arange(n + 2, dtype=np.uint32)
+    ga, gs = e.pos_to_loc(np.full(pos.shape, doc, np.uint32), pos)
+    oa, os_ = o.pos_to_loc(pos)
+    assert np.array_equal(ga, oa) and np.array_equal(gs, os_)
+    s = o.sizes()
+    for a in range(s["agents"]):
+        seq = np.arange(s["next_order"] + 1, dtype=np.uint32)
+        ag = np.full(seq.shape, a, np.uint16)
+        gp, gd = e.loc_to_pos(np.full(seq.shape, doc, np.uint32), ag, seq)
+        op, od = o.loc_to_pos(ag, seq)
+        assert np.array_equal(gd, od)
+        assert np.array_equal(gp[od != 2], op[od != 2])
+
+
+@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode", "automerge-paper"])
+def test_trace_local_exact(name):
+    t = load_trace(name)
+    e = crdt_amd.Engine(1, 32)
+    a = e.agent_intern([0], ["jeremy"])
+    st = e.apply_trace([0], int(a[0]), t.counts, t.patches)
+    assert st[0] == 0
+    o = OracleDoc(32, 16)
+    o.apply_trace(o.agent("jeremy"), t.counts, t.patches)
+    assert_same(e.export(0), o.export())
+    assert int(e.digests()[0]) == o.digest()
+    assert int(e.lens()[0]) == t.end_len
+    check_queries(e, 0, o)
+
+
+@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode", "automerge-paper"])
+def test_trace_remote_exact(name):
+    w = load_remote_wire(name)
+    e = crdt_amd.Engine(2, 32)
+    st = e.apply_remote_wire([0, 1], [w, w])
+    assert (st == 0).all()
+    o = OracleDoc(32, 16)
+    assert o.apply_remote_wire(w) == 0
+    for d in (0, 1):
+        assert_same(e.export(d), o.export())
+    assert (e.digests() == np.uint64(o.digest())).all()
+    check_queries(e, 1, o)
+
+
+@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode"])
+def test_trace_debug_layout(name):
+    t = load_trace(name)
+    e = crdt_amd.Engine(1, 4)
+    a = e.agent_intern([0], ["jeremy"])
+    assert e.apply_trace([0], int(a[0]), t.counts, t.patches)[0] == 0
+    o = OracleDoc(4, 8)
+    o.apply_trace(o.agent("jeremy"), t.counts, t.patches)
+    assert_same(e.export(0), o.export())
+
+
+def test_mixed_corpus_and_random():
+    # documents with different traces and random edit streams in one launch (segmented work)
+    names = ["sveltecomponent", "rustcode", "automerge-paper"]
+    traces = [load_trace(n) for n in names]
+    rnd = [random_local_trace(1000 + i, 3000) for i in range(5)]
+    docs = [(t.counts, t.patches) for t in traces] + rnd
+    e = crdt_amd.Engine(len(docs), 32)
+    ag = e.agent_intern(list(range(len(docs))), ["jeremy"] * len(docs))
+    per_doc = []
+    for i, (c, p) in enumerate(docs):
+        off = np.concatenate([[0], np.cumsum(c)]).astype(int)
+        per_doc.append((i, [(int(ag[i]), p[off[k]:off[k + 1]]) for k in range(len(c))]))
+    st = e.apply_local(per_doc)
+    assert (st == 0).all(), st
+    dg = e.digests()
+    for i, (c, p) in enumerate(docs):
+        o = OracleDoc()
+        o.apply_trace(o.agent("jeremy"), c, p)
+        assert int(dg[i]) == o.digest(), i
+        if i >= 3:
+            assert_same(e.export(i), o.export())
+
+
+def test_reference_unit_cases():
+    from test_oracle import wire, ROOT_ID
+    # remote_txns (doc.rs:620-676)
+    e = crdt_amd.Engine(2, 4)
+    w1 = wire([("seph", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 2)])])
+    w2 = wire([("seph", 2, [("seph", 1)], [("del", ("seph", 0), 2)])])
+    assert e.apply_remote_wire([0], [w1])[0] == 0
+    assert e.apply_remote_wire([0], [w2])[0] == 0
+    o = OracleDoc(4, 8)
+    o.apply_remote_wire(w1)
+    o.apply_remote_wire(w2)
+    assert_same(e.export(0), o.export())
+    # smoke (doc.rs:522-532) + deletes_merged (doc.rs:589-601) on doc 1, several apply calls
+    a = int(e.agent_intern([1], ["seph"])[0])
+    for ops in ([(0, 0, 2)], [(1, 0, 4)], [(0, 3, 0)], [(0, 0, 3)], [(0, 1, 0)], [(0, 1, 0)], [(0, 1, 0)]):
+        assert e.apply_local([(1, [(a, ops)])])[0] == 0
+    o = OracleDoc(4, 8)
+    oa = o.agent("seph")
+    for ops in ([(0, 0, 2)], [(1, 0, 4)], [(0, 3, 0)], [(0, 0, 3)], [(0, 1, 0)], [(0, 1, 0)], [(0, 1, 0)]):
+        o.apply_local(oa, ops)
+    assert_same(e.export(1), o.export())
+
+
+def test_error_statuses_match():
+    from test_oracle import wire, ROOT_ID
+    cases = [
+        wire([("seph", 1, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 1)])]),                     # SEQ
+        wire([("A", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 2)]),
+              ("B", 0, [("A", 0)], [("ins", ("A", 0), ROOT_ID, 1)])]),                        # NONTERMINATING
+        wire([("A", 0, [ROOT_ID], [("ins", ("Z", 0), ROOT_ID, 1)])]),                         # UNKNOWN_AGENT
+        wire([("A", 0, [ROOT_ID], [("ins", ROOT_ID, ROOT_ID, 2)]),
+              ("A", 2, [("A", 1)], [("del", ("A", 7), 1)])]),                                 # UNKNOWN_ID
+    ]
+    e = crdt_amd.Engine(len(cases), 32)
+    st = e.apply_remote_wire(list(range(len(cases))), cases)
+    exp = []
+    for w in cases:
+        o = OracleDoc()
+        exp.append(o.apply_remote_wire(w))
+    assert list(st) == exp, (list(st), exp)
+    assert exp == [-2, -5, -3, -4]
+
+
+def test_concurrent_histories():
+    from fuzz_gen import concurrent_wire
+    wires = [concurrent_wire(s, n_agents=3, rounds=5)[0] for s in range(6)]
+    e = crdt_amd.Engine(len(wires), 32)
+    st = e.apply_remote_wire(list(range(len(wires))), wires)
+    dg = e.digests()
+    for i, w in enumerate(wires):
+        o = OracleDoc()
+        so = o.apply_remote_wire(w)
+        assert st[i] == so, (i, st[i], so)
+        if so == 0:
+            assert int(dg[i]) == o.digest()
+            assert_same(e.export(i), o.export())

@@ -1,0 +1,318 @@
+"""crdt_amd — Python binding of the MI355X list-CRDT engine (include/crdt_gpu.h).
+
+The product is the C ABI library text-crdt-rust_amd/build/libcrdt_gpu.so (HIP kernels for gfx950 +
+C++ host).  This module is a thin ctypes layer used by tests and bench.py; it mirrors the
+reference's `ListCRDT` surface (src/list/doc.rs) for one document (`ListCRDT`) and exposes the
+batched many-document form (`Engine`).  There is no CPU fallback: without the built library or a
+gfx950 device every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Iterable, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(PKG_DIR)
+REPO = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "build", "libcrdt_gpu.so")
+CSRC = os.path.join(PKG_ROOT, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+
+OK = 0
+STATUS_NAMES = {0: "OK", -1: "POS_OOB", -2: "SEQ", -3: "UNKNOWN_AGENT", -4: "UNKNOWN_ID", -5: "NONTERMINATING",
+                -6: "CAPACITY", -7: "EMPTY_TXN", -8: "FRONTIER", -9: "BAD_INPUT", -10: "INTERNAL"}
+ROOT_AGENT = 0xFFFF
+ROOT_ORDER = 0xFFFFFFFF
+
+
+class CrdtError(RuntimeError):
+    pass
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile libcrdt_gpu.so for gfx950 with hipcc (in-tree)."""
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "crdt_gpu.h")]
+    if not force and os.path.exists(LIB_PATH):
+        lt = os.path.getmtime(LIB_PATH)
+        if all(os.path.getmtime(s) <= lt for s in srcs):
+            return LIB_PATH
+    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-fno-strict-aliasing", "-I" + INCLUDE, "-I" + CSRC, "-o", LIB_PATH + ".tmp",
+           os.path.join(CSRC, "engine.hip")]
+    r = subprocess.run(cmd, capture_output=not verbose, text=True)
+    if r.returncode != 0:
+        raise CrdtError("hipcc failed:\n" + (r.stderr or "")[-4000:])
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CrdtError(f"{LIB_PATH} not built (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
+    P = C.POINTER
+
+    class Cfg(C.Structure):
+        _fields_ = [("leaf_cap", C.c_uint32), ("device", C.c_int32)]
+    L.Cfg = Cfg
+    L.crdt_engine_create.argtypes = [P(Cfg), P(vp)]
+    L.crdt_engine_destroy.argtypes = [vp]
+    L.crdt_docs_alloc.argtypes = [vp, u64]
+    L.crdt_num_docs.argtypes = [vp]
+    L.crdt_num_docs.restype = u64
+    L.crdt_agent_intern.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(C.c_uint16)]
+    L.crdt_apply_local.argtypes = [vp, u64, P(u32), P(u64), vp, vp, P(i32)]
+    L.crdt_stage_local.argtypes = [vp, u64, P(u32), P(u64), vp, vp]
+    L.crdt_apply_remote_wire.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(u64), P(i32)]
+    L.crdt_stage_remote_wire.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(u64)]
+    L.crdt_stage_remote_replicated.argtypes = [vp, C.c_char_p, u64, u32, P(C.c_char_p)]
+    L.crdt_reset_async.argtypes = [vp]
+    L.crdt_run.argtypes = [vp, P(i32)]
+    L.crdt_run_async.argtypes = [vp]
+    L.crdt_publish_async.argtypes = [vp]
+    L.crdt_sync.argtypes = [vp]
+    L.crdt_pos_to_loc.argtypes = [vp, u64, P(u32), P(u32), P(C.c_uint16), P(u32)]
+    L.crdt_loc_to_pos.argtypes = [vp, u64, P(u32), P(C.c_uint16), P(u32), P(u32), P(C.c_uint8)]
+    L.crdt_pos_to_loc_dev_async.argtypes = [vp, u64, vp, vp, vp, vp]
+    L.crdt_loc_to_pos_dev_async.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+    L.crdt_doc_len.argtypes = [vp, u64, P(u32), P(u32)]
+    L.crdt_doc_status.argtypes = [vp, P(i32)]
+    L.crdt_digest.argtypes = [vp, P(u64)]
+    L.crdt_export_sizes.argtypes = [vp, u32, P(u64)]
+    L.crdt_export.argtypes = [vp, u32] + [P(u32)] * 9
+    L.crdt_last_timings.argtypes = [vp, P(C.c_double), P(C.c_double)]
+    L.crdt_stream.argtypes = [vp]
+    L.crdt_stream.restype = vp
+    L.crdt_last_error.restype = C.c_char_p
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = [
+    "crdt_engine_create", "crdt_engine_destroy", "crdt_docs_alloc", "crdt_num_docs", "crdt_agent_intern",
+    "crdt_apply_local", "crdt_apply_remote_wire", "crdt_stage_local", "crdt_stage_remote_wire",
+    "crdt_stage_remote_replicated", "crdt_reset_async", "crdt_run", "crdt_run_async", "crdt_publish_async",
+    "crdt_sync", "crdt_pos_to_loc", "crdt_loc_to_pos", "crdt_pos_to_loc_dev_async", "crdt_loc_to_pos_dev_async",
+    "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
+    "crdt_stream", "crdt_last_error",
+]
+
+
+def _p(a, t=C.c_uint32):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        err = lib().crdt_last_error()
+        raise CrdtError(f"{what} failed rc={rc} {err.decode() if err else ''}")
+
+
+class Engine:
+    """Many documents on one MI355X.  Mirrors ListCRDT per document (index `doc`)."""
+
+    def __init__(self, n_docs: int, leaf_cap: int = 32, device: int = 0):
+        L = lib()
+        self.L = L
+        self.h = C.c_void_p()
+        cfg = L.Cfg(leaf_cap, device)
+        _check(L.crdt_engine_create(C.byref(cfg), C.byref(self.h)), "crdt_engine_create")
+        _check(L.crdt_docs_alloc(self.h, n_docs), "crdt_docs_alloc")
+        self.n_docs = n_docs
+        self.leaf_cap = leaf_cap
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.L.crdt_engine_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- ListCRDT::get_or_create_agent_id (doc.rs:66-80)
+    def agent_intern(self, docs: Sequence[int], names: Sequence[str]) -> np.ndarray:
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        out = np.zeros(len(names), np.uint16)
+        _check(self.L.crdt_agent_intern(self.h, len(names), _p(d), arr, _p(out, C.c_uint16)), "agent_intern")
+        return out
+
+    @staticmethod
+    def _local_arrays(per_doc):
+        """per_doc: list of (doc, [(agent, ops[(pos,del,ins)...]), ...])."""
+        docs, txn_off, txns, ops = [], [0], [], []
+        for doc, tx in per_doc:
+            docs.append(doc)
+            for agent, o in tx:
+                o = np.asarray(o, dtype=np.uint32).reshape(-1, 3)
+                txns.append((agent, o.shape[0]))
+                ops.append(o)
+            txn_off.append(len(txns))
+        return (np.array(docs, np.uint32), np.array(txn_off, np.uint64),
+                np.array(txns, np.uint32).reshape(-1, 2),
+                np.concatenate(ops).astype(np.uint32) if ops else np.zeros((0, 3), np.uint32))
+
+    def apply_local(self, per_doc) -> np.ndarray:
+        d, off, tx, ops = self._local_arrays(per_doc)
+        st = np.zeros(d.shape[0], np.int32)
+        _check(self.L.crdt_apply_local(self.h, d.shape[0], _p(d), _p(off, C.c_uint64), tx.ctypes.data,
+                                       ops.ctypes.data, _p(st, C.c_int32)), "apply_local")
+        return st
+
+    def apply_trace(self, docs: Sequence[int], agent: int | Sequence[int], counts: np.ndarray, patches: np.ndarray,
+                    stage_only: bool = False) -> np.ndarray:
+        """Apply the same trace (txn patch counts + patches) to every doc in `docs`."""
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        n = d.shape[0]
+        counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        agents = np.broadcast_to(np.asarray(agent, dtype=np.uint32), (n,))
+        tx = np.zeros((n * counts.shape[0], 2), np.uint32)
+        for i in range(n):
+            tx[i * counts.shape[0]:(i + 1) * counts.shape[0], 0] = agents[i]
+            tx[i * counts.shape[0]:(i + 1) * counts.shape[0], 1] = counts
+        off = (np.arange(n + 1, dtype=np.uint64) * counts.shape[0]).astype(np.uint64)
+        ops = np.ascontiguousarray(np.tile(np.asarray(patches, np.uint32).reshape(-1, 3), (n, 1)))
+        if stage_only:
+            _check(self.L.crdt_stage_local(self.h, n, _p(d), _p(off, C.c_uint64), tx.ctypes.data, ops.ctypes.data),
+                   "stage_local")
+            return np.zeros(n, np.int32)
+        st = np.zeros(n, np.int32)
+        _check(self.L.crdt_apply_local(self.h, n, _p(d), _p(off, C.c_uint64), tx.ctypes.data, ops.ctypes.data,
+                                       _p(st, C.c_int32)), "apply_local")
+        return st
+
+    def apply_remote_wire(self, docs: Sequence[int], wires: Sequence[bytes], stage_only: bool = False) -> np.ndarray:
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        arr = (C.c_char_p * len(wires))(*wires)
+        ln = np.array([len(w) for w in wires], np.uint64)
+        if stage_only:
+            _check(self.L.crdt_stage_remote_wire(self.h, d.shape[0], _p(d), arr, _p(ln, C.c_uint64)), "stage_remote")
+            return np.zeros(d.shape[0], np.int32)
+        st = np.zeros(d.shape[0], np.int32)
+        _check(self.L.crdt_apply_remote_wire(self.h, d.shape[0], _p(d), arr, _p(ln, C.c_uint64), _p(st, C.c_int32)),
+               "apply_remote_wire")
+        return st
+
+    def stage_remote_replicated(self, wire: bytes, rename_idx: int, names: Sequence[str]):
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        _check(self.L.crdt_stage_remote_replicated(self.h, wire, len(wire), rename_idx, arr), "stage_replicated")
+
+    def reset_async(self):
+        _check(self.L.crdt_reset_async(self.h), "reset")
+
+    def run(self) -> np.ndarray:
+        st = np.zeros(self.n_docs, np.int32)
+        _check(self.L.crdt_run(self.h, _p(st, C.c_int32)), "run")
+        return st
+
+    def run_async(self):
+        _check(self.L.crdt_run_async(self.h), "run_async")
+
+    def publish_async(self):
+        _check(self.L.crdt_publish_async(self.h), "publish")
+
+    def sync(self):
+        _check(self.L.crdt_sync(self.h), "sync")
+
+    def status(self) -> np.ndarray:
+        st = np.zeros(self.n_docs, np.int32)
+        _check(self.L.crdt_doc_status(self.h, _p(st, C.c_int32)), "status")
+        return st
+
+    def lens(self, docs=None) -> np.ndarray:
+        d = np.arange(self.n_docs, dtype=np.uint32) if docs is None else np.ascontiguousarray(docs, dtype=np.uint32)
+        out = np.zeros(d.shape[0], np.uint32)
+        _check(self.L.crdt_doc_len(self.h, d.shape[0], _p(d), _p(out)), "doc_len")
+        return out
+
+    def digests(self) -> np.ndarray:
+        out = np.zeros(self.n_docs, np.uint64)
+        _check(self.L.crdt_digest(self.h, _p(out, C.c_uint64)), "digest")
+        return out
+
+    def pos_to_loc(self, docs, pos):
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        p = np.ascontiguousarray(pos, dtype=np.uint32)
+        a = np.zeros(p.shape[0], np.uint16)
+        s = np.zeros(p.shape[0], np.uint32)
+        _check(self.L.crdt_pos_to_loc(self.h, p.shape[0], _p(d), _p(p), _p(a, C.c_uint16), _p(s)), "pos_to_loc")
+        return a, s
+
+    def loc_to_pos(self, docs, agent, seq):
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        a = np.ascontiguousarray(agent, dtype=np.uint16)
+        s = np.ascontiguousarray(seq, dtype=np.uint32)
+        p = np.zeros(s.shape[0], np.uint32)
+        dl = np.zeros(s.shape[0], np.uint8)
+        _check(self.L.crdt_loc_to_pos(self.h, s.shape[0], _p(d), _p(a, C.c_uint16), _p(s), _p(p), _p(dl, C.c_uint8)),
+               "loc_to_pos")
+        return p, dl
+
+    def export(self, doc: int) -> dict:
+        s = np.zeros(12, np.uint64)
+        _check(self.L.crdt_export_sizes(self.h, doc, _p(s, C.c_uint64)), "export_sizes")
+        n = [int(x) for x in s]
+        raw = np.zeros((n[0], 4), np.uint32)
+        ls = np.zeros(n[1], np.uint32)
+        canon = np.zeros((n[2], 4), np.uint32)
+        cwo = np.zeros((n[3], 4), np.uint32)
+        dl = np.zeros((n[4], 3), np.uint32)
+        dd = np.zeros((n[5], 3), np.uint32)
+        tx = np.zeros((n[6], 5), np.uint32)
+        pa = np.zeros(n[7], np.uint32)
+        fr = np.zeros(n[8], np.uint32)
+        _check(self.L.crdt_export(self.h, doc, _p(raw), _p(ls), _p(canon), _p(cwo), _p(dl), _p(dd), _p(tx), _p(pa),
+                                  _p(fr)), "export")
+        return dict(raw=raw, leaf_sizes=ls, canon=canon, cwo=cwo, deletes=dl, dd=dd, txns=tx, parents=pa,
+                    frontier=fr, len=n[11], next_order=n[10])
+
+    def timings(self):
+        a, b = C.c_double(), C.c_double()
+        self.L.crdt_last_timings(self.h, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def stream(self) -> int:
+        return self.L.crdt_stream(self.h) or 0
+
+
+class ListCRDT:
+    """One document with the reference's method names (src/list/doc.rs), on its own engine."""
+
+    def __init__(self, leaf_cap: int = 32, device: int = 0):
+        self.e = Engine(1, leaf_cap, device)
+
+    def get_or_create_agent_id(self, name: str) -> int:         # doc.rs:66
+        return int(self.e.agent_intern([0], [name])[0])
+
+    def apply_local_txn(self, agent: int, ops) -> int:          # doc.rs:376
+        return int(self.e.apply_local([(0, [(agent, ops)])])[0])
+
+    def local_insert(self, agent: int, pos: int, ins_len: int) -> int:   # doc.rs:472
+        return self.apply_local_txn(agent, [(pos, 0, ins_len)])
+
+    def local_delete(self, agent: int, pos: int, del_span: int) -> int:  # doc.rs:478
+        return self.apply_local_txn(agent, [(pos, del_span, 0)])
+
+    def apply_remote_wire(self, wire: bytes) -> int:            # doc.rs:242 (batch of RemoteTxn)
+        return int(self.e.apply_remote_wire([0], [wire])[0])
+
+    def __len__(self) -> int:                                   # doc.rs:484
+        return int(self.e.lens([0])[0])
+
+    def status(self) -> int:
+        return int(self.e.status()[0])

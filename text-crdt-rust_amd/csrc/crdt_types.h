@@ -122,6 +122,7 @@ struct DocState {
   u32 ng, next_order, len, n_cwo;
   u32 n_del, n_dd, n_txn, n_par;
   u32 n_fr, n_agents, n_items, cap_need;
+  u32 n_entries, pad0, pad1, pad2;
 };
 
 struct Pools {

@@ -1,0 +1,825 @@
+// MI355X list-CRDT engine: host side (pool allocation, staging, growth) + the C ABI of
+// include/crdt_gpu.h.  All compute runs in the HIP kernels of kernels.h; there is no CPU
+// fallback: without a usable gfx950 device every entry point returns CRDT_E_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "crdt_gpu.h"
+#include "host_plan.h"
+#include "kernels.h"
+
+using namespace crdt;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+#define HIPCHK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess) {                                                             \
+      g_last_error = std::string(#x) + ": " + hipGetErrorString(e_);                    \
+      return CRDT_E_DEVICE;                                                             \
+    }                                                                                   \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T*& p, u64 n) {
+  p = nullptr;
+  if (n == 0) n = 1;
+  return hipMalloc((void**)&p, sizeof(T) * n);
+}
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+// Relocatable per-document pools (sized by the per-document capacities).
+struct PoolSet {
+  Span* leaves = nullptr;
+  u32* sol = nullptr;
+  u32* dir_leaf = nullptr;
+  u32* dir_vis = nullptr;
+  u32* leaf_of = nullptr;
+  CwoRun* cwo = nullptr;
+  ARun* arun = nullptr;
+  DelRun* dels = nullptr;
+  DDRun* dd = nullptr;
+  TxnRec* txns = nullptr;
+  u32* parents = nullptr;
+  AgentRec* agents = nullptr;
+  Span* canon = nullptr;
+  u32* vpos = nullptr;
+  u32* span_of = nullptr;
+  u64 bytes = 0;
+  void free_all() {
+    dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(cwo); dfree(arun);
+    dfree(dels); dfree(dd); dfree(txns); dfree(parents); dfree(agents); dfree(canon); dfree(vpos); dfree(span_of);
+    bytes = 0;
+  }
+};
+
+struct DocHost {
+  AgentTable agents;
+  StreamNeeds cum;          // cumulative needs of everything applied since the last reset
+  Caps caps{};              // current capacities
+  std::vector<u32> agent_cap;
+  bool sized = false;
+};
+
+}  // namespace
+
+struct crdt_engine {
+  u32 L = 32;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  u64 n_docs = 0;
+  std::vector<DocHost> docs;
+  std::vector<DocSeg> seg_h;
+  std::vector<DocState> st_h;
+  // fixed per-document buffers
+  DocState* st = nullptr;
+  DocSeg* segs = nullptr;
+  u32* frontier = nullptr;
+  GroupRec* groups = nullptr;
+  u32* canon_n = nullptr;
+  u32* len = nullptr;
+  u64* digest = nullptr;
+  u32* n_agents_d = nullptr;
+  PoolSet pools;
+  Rec* recs = nullptr;
+  u64 rec_cap = 0;
+  bool published = false;
+  double last_replay_ms = 0, last_publish_ms = 0;
+  // query scratch
+  void* qbuf = nullptr;
+  u64 qbuf_bytes = 0;
+
+  Pools pools_view(const PoolSet& ps) const {
+    Pools p{};
+    p.leaves = ps.leaves;
+    p.dir_leaf = ps.dir_leaf;
+    p.dir_vis = ps.dir_vis;
+    p.slot_of_leaf = ps.sol;
+    p.leaf_of = ps.leaf_of;
+    p.cwo = ps.cwo;
+    p.arun = ps.arun;
+    p.dels = ps.dels;
+    p.dd = ps.dd;
+    p.txns = ps.txns;
+    p.parents = ps.parents;
+    p.frontier = frontier;
+    p.agents = ps.agents;
+    p.groups = groups;
+    p.recs = recs;
+    p.seg = segs;
+    p.st = st;
+    return p;
+  }
+  PubOut pub_view() const {
+    PubOut o{};
+    o.canon = pools.canon;
+    o.vpos = pools.vpos;
+    o.span_of = pools.span_of;
+    o.canon_n = canon_n;
+    o.len = len;
+    o.digest = digest;
+    return o;
+  }
+
+  void release() {
+    pools.free_all();
+    dfree(st); dfree(segs); dfree(frontier); dfree(groups); dfree(canon_n); dfree(len); dfree(digest); dfree(n_agents_d);
+    dfree(recs);
+    rec_cap = 0;
+    if (qbuf) (void)hipFree(qbuf);
+    qbuf = nullptr;
+    qbuf_bytes = 0;
+  }
+
+  int set_device() {
+    HIPCHK(hipSetDevice(device));
+    return 0;
+  }
+
+  int alloc_docs(u64 n) {
+    int r = set_device();
+    if (r) return r;
+    HIPCHK(hipStreamSynchronize(stream));
+    release();
+    n_docs = n;
+    docs.assign(n, DocHost{});
+    seg_h.assign(n, DocSeg{});
+    st_h.assign(n, DocState{});
+    HIPCHK(dalloc(st, n));
+    HIPCHK(dalloc(segs, n));
+    HIPCHK(dalloc(frontier, n * FRONTIER_CAP));
+    HIPCHK(dalloc(groups, n * MAX_GROUPS));
+    HIPCHK(dalloc(canon_n, n));
+    HIPCHK(dalloc(len, n));
+    HIPCHK(dalloc(digest, n));
+    HIPCHK(dalloc(n_agents_d, n));
+    HIPCHK(hipMemsetAsync(st, 0, sizeof(DocState) * std::max<u64>(n, 1), stream));
+    // size every document for an empty stream and initialise it
+    for (u64 d = 0; d < n; d++) docs[d].caps = plan_caps(StreamNeeds{}, 0, true, 48);
+    r = layout(false);
+    if (r) return r;
+    return init_all();
+  }
+
+  // Assign per-document bases from docs[].caps into a fresh PoolSet; if `move`, relocate the
+  // existing state into it (k_relayout), else just install it.
+  int layout(bool move) {
+    PoolSet np;
+    u64 nl = 0, nb = 0, nm = 0, nc = 0, na = 0, ndl = 0, ndd = 0, nt = 0, npar = 0, nag = 0;
+    std::vector<DocSeg> nseg(n_docs);
+    std::vector<AgentRec> agent_tab;
+    std::vector<u32> n_agents(n_docs);
+    for (u64 d = 0; d < n_docs; d++) {
+      DocHost& h = docs[d];
+      const Caps& c = h.caps;
+      DocSeg s{};
+      s.leaf_base = nl; s.leaf_cap = c.leaf; nl += c.leaf;
+      s.blk_base = nb; s.blk_cap = c.blk; nb += c.blk;
+      s.map_base = nm; s.map_cap = c.map; nm += c.map;
+      s.cwo_base = nc; s.cwo_cap = c.cwo; nc += c.cwo;
+      s.del_base = ndl; s.del_cap = c.del; ndl += c.del;
+      s.dd_base = ndd; s.dd_cap = c.dd; ndd += c.dd;
+      s.txn_base = nt; s.txn_cap = c.txn; nt += c.txn;
+      s.par_base = npar; s.par_cap = c.par; npar += c.par;
+      s.fr_base = d * FRONTIER_CAP;
+      s.grp_base = d * MAX_GROUPS;
+      s.agent_base = nag;
+      u32 ag = (u32)h.agents.names.size();
+      s.agent_cap = ag;
+      n_agents[d] = ag;
+      s.arun_base = na;
+      std::vector<u32> rk = h.agents.ranks();
+      u32 rb = 0;
+      h.agent_cap.resize(ag, 0);
+      for (u32 a = 0; a < ag; a++) {
+        u32 t = a < h.cum.txns_per_agent.size() ? h.cum.txns_per_agent[a] : 0;
+        u32 need = std::min<u32>(t + 1, 64 + t / 64);
+        if (h.agent_cap[a] < need) h.agent_cap[a] = need;
+        agent_tab.push_back(AgentRec{rb, 0, h.agent_cap[a], rk[a]});
+        rb += h.agent_cap[a];
+      }
+      s.arun_cap = rb;
+      na += rb;
+      nag += ag;
+      s.flags = DOC_TRACK_MAP;
+      s.rec_base = seg_h[d].rec_base;
+      s.rec_n = seg_h[d].rec_n;
+      nseg[d] = s;
+    }
+    HIPCHK(dalloc(np.leaves, nl * L));
+    HIPCHK(dalloc(np.sol, nl));
+    HIPCHK(dalloc(np.dir_leaf, nb * GROUP));
+    HIPCHK(dalloc(np.dir_vis, nb * GROUP));
+    HIPCHK(dalloc(np.leaf_of, nm));
+    HIPCHK(dalloc(np.span_of, nm));
+    HIPCHK(dalloc(np.cwo, nc));
+    HIPCHK(dalloc(np.arun, na));
+    HIPCHK(dalloc(np.dels, ndl));
+    HIPCHK(dalloc(np.dd, ndd));
+    HIPCHK(dalloc(np.txns, nt));
+    HIPCHK(dalloc(np.parents, npar));
+    HIPCHK(dalloc(np.agents, nag));
+    HIPCHK(dalloc(np.canon, nl * L));
+    HIPCHK(dalloc(np.vpos, nl * L));
+    np.bytes = nl * L * (16 + 16 + 4) + nl * 4 + nb * GROUP * 8 + nm * 8 + nc * 16 + na * 16 + ndl * 12 + ndd * 12 +
+               nt * 32 + npar * 4 + nag * 16;
+    if (!agent_tab.empty())
+      HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(n_agents_d, n_agents.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
+    DocSeg* old_segs = nullptr;
+    if (move) {
+      HIPCHK(dalloc(old_segs, n_docs));
+      HIPCHK(hipMemcpyAsync(old_segs, segs, n_docs * sizeof(DocSeg), hipMemcpyDeviceToDevice, stream));
+    }
+    HIPCHK(hipMemcpyAsync(segs, nseg.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
+    if (move) {
+      Pools src = pools_view(pools), dst = pools_view(np);
+      if (L == 32) hipLaunchKernelGGL(k_relayout<32>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs);
+      else hipLaunchKernelGGL(k_relayout<4>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipStreamSynchronize(stream));
+      dfree(old_segs);
+    } else {
+      HIPCHK(hipStreamSynchronize(stream));
+    }
+    pools.free_all();
+    pools = np;
+    seg_h = nseg;
+    published = false;
+    return 0;
+  }
+
+  int init_all() {
+    // host-side agent counts into the state before k_init (k_init keeps n_agents)
+    int r = push_agent_counts();
+    if (r) return r;
+    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (n_docs) {
+      if (L == 32) hipLaunchKernelGGL(k_init<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
+      else hipLaunchKernelGGL(k_init<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
+      HIPCHK(hipGetLastError());
+    }
+    published = false;
+    return 0;
+  }
+
+  int push_agent_counts() {
+    // write st[d].n_agents (field offset) for every document
+    std::vector<u32> na(n_docs);
+    for (u64 d = 0; d < n_docs; d++) na[d] = (u32)docs[d].agents.names.size();
+    HIPCHK(hipMemcpyAsync(n_agents_d, na.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
+    for (u64 d = 0; d < n_docs; d++) {
+      HIPCHK(hipMemcpyAsync((char*)(st + d) + offsetof(DocState, n_agents), n_agents_d + d, 4, hipMemcpyDeviceToDevice, stream));
+    }
+    return 0;
+  }
+
+  // Stage per-document record streams (host-encoded) and grow capacities if needed.
+  int stage(const std::vector<u64>& doc_ids, std::vector<const std::vector<Rec>*>& streams, std::vector<StreamNeeds>& needs) {
+    int r = set_device();
+    if (r) return r;
+    HIPCHK(hipStreamSynchronize(stream));
+    // cumulative needs -> capacities
+    bool grow = false;
+    for (size_t i = 0; i < doc_ids.size(); i++) {
+      DocHost& h = docs[doc_ids[i]];
+      StreamNeeds& c = h.cum;
+      const StreamNeeds& n = needs[i];
+      c.n_txn += n.n_txn; c.n_ltxn += n.n_ltxn; c.n_rtxn += n.n_rtxn; c.n_ops += n.n_ops; c.orders += n.orders;
+      c.local_del += n.local_del; c.remote_del_ops += n.remote_del_ops; c.remote_parents += n.remote_parents;
+      if (c.txns_per_agent.size() < n.txns_per_agent.size()) c.txns_per_agent.resize(n.txns_per_agent.size(), 0);
+      for (size_t a = 0; a < n.txns_per_agent.size(); a++) c.txns_per_agent[a] += n.txns_per_agent[a];
+      Caps nc = plan_caps(c, (u32)h.agents.names.size(), true, 48);
+      Caps& oc = h.caps;
+      auto up = [&](u32& o, u32 v) { if (v > o) { o = v; grow = true; } };
+      up(oc.leaf, nc.leaf); up(oc.blk, nc.blk); up(oc.map, nc.map); up(oc.cwo, nc.cwo); up(oc.arun, nc.arun);
+      up(oc.del, nc.del); up(oc.dd, nc.dd); up(oc.txn, nc.txn); up(oc.par, nc.par); up(oc.agent, nc.agent);
+      for (size_t a = 0; a < h.agents.names.size(); a++) {
+        u32 t = a < c.txns_per_agent.size() ? c.txns_per_agent[a] : 0;
+        u32 need = std::min<u32>(t + 1, 64 + t / 64);
+        if (a >= h.agent_cap.size() || h.agent_cap[a] < need) grow = true;
+      }
+      if (h.agents.names.size() != h.agent_cap.size()) grow = true;
+    }
+    // records: one buffer for this call
+    u64 total = 0;
+    for (auto* s : streams) total += s->size();
+    if (total > rec_cap) {
+      dfree(recs);
+      rec_cap = std::max<u64>(total, 1024);
+      HIPCHK(dalloc(recs, rec_cap));
+    }
+    for (auto& sg : seg_h) { sg.rec_base = 0; sg.rec_n = 0; }
+    u64 off = 0;
+    const std::vector<Rec>* prev = nullptr;
+    u64 prev_off = 0;
+    for (size_t i = 0; i < doc_ids.size(); i++) {
+      DocSeg& sg = seg_h[doc_ids[i]];
+      const std::vector<Rec>& sv = *streams[i];
+      sg.rec_base = off;
+      sg.rec_n = (u32)sv.size();
+      if (!sv.empty()) {
+        if (&sv == prev)  // replicated stream: device-to-device copy of the previous upload
+          HIPCHK(hipMemcpyAsync(recs + off, recs + prev_off, sv.size() * sizeof(Rec), hipMemcpyDeviceToDevice, stream));
+        else
+          HIPCHK(hipMemcpyAsync(recs + off, sv.data(), sv.size() * sizeof(Rec), hipMemcpyHostToDevice, stream));
+        HIPCHK(hipStreamSynchronize(stream));
+      }
+      prev = &sv;
+      prev_off = off;
+      off += sv.size();
+    }
+    if (grow) {
+      r = layout(true);
+      if (r) return r;
+    } else {
+      HIPCHK(hipMemcpyAsync(segs, seg_h.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
+      r = push_agent_counts();
+      if (r) return r;
+    }
+    if (n_docs) {
+      hipLaunchKernelGGL(k_reset_recpos, dim3((u32)((n_docs + 255) / 256)), dim3(256), 0, stream, st, (u32)n_docs, 0u);
+      HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(stream));
+    published = false;
+    return 0;
+  }
+
+  int launch_replay() {
+    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (!n_docs) return 0;
+    if (L == 32) hipLaunchKernelGGL(k_replay<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
+    else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
+    HIPCHK(hipGetLastError());
+    published = false;
+    return 0;
+  }
+
+  int pull_states() {
+    HIPCHK(hipMemcpyAsync(st_h.data(), st, n_docs * sizeof(DocState), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    return 0;
+  }
+
+  // Replay with growth: on ST_NEED_CAPACITY grow the flagged tables and resume.
+  int run(int32_t* status_out) {
+    int r = set_device();
+    if (r) return r;
+    for (int iter = 0; iter < 40; iter++) {
+      HIPCHK(hipEventRecord(ev[0], stream));
+      r = launch_replay();
+      if (r) return r;
+      HIPCHK(hipEventRecord(ev[1], stream));
+      r = pull_states();
+      if (r) return r;
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+      last_replay_ms = ms;
+      bool any = false;
+      for (u64 d = 0; d < n_docs; d++) {
+        if (st_h[d].status != ST_NEED_CAPACITY) continue;
+        any = true;
+        Caps& c = docs[d].caps;
+        u32 need = st_h[d].cap_need;
+        if (need & 1u) {
+          if (c.leaf >= MAX_LEAVES) { need &= ~1u; }
+          c.leaf = std::min<u32>(c.leaf * 2, MAX_LEAVES);
+          c.blk = c.leaf / 32 + 2;
+        }
+        if (need & 2u) { c.cwo = c.cwo * 2 + 1; c.txn = c.txn * 2 + 1; }
+        if (need & 4u) c.del = c.del * 2 + 16;
+        if (need & 8u) c.par = c.par * 2 + 16;
+        if (need & 16u) c.map = c.map * 2 + 16;
+        if (need & 32u) for (auto& x : docs[d].agent_cap) x = x * 2 + 1;
+        if (need == 0) {  // cannot grow: make it a hard capacity error
+          DocState s = st_h[d];
+          s.status = ST_CAPACITY;
+          HIPCHK(hipMemcpyAsync(&st[d].status, &s.status, 4, hipMemcpyHostToDevice, stream));
+        }
+      }
+      if (!any) break;
+      r = layout(true);
+      if (r) return r;
+    }
+    if (status_out)
+      for (u64 d = 0; d < n_docs; d++) status_out[d] = st_h[d].status == ST_NEED_CAPACITY ? ST_CAPACITY : st_h[d].status;
+    return 0;
+  }
+
+  int publish() {
+    int r = set_device();
+    if (r) return r;
+    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (!n_docs) return 0;
+    HIPCHK(hipEventRecord(ev[2], stream));
+    if (L == 32) hipLaunchKernelGGL(k_publish<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
+    else hipLaunchKernelGGL(k_publish<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev[3], stream));
+    published = true;
+    return 0;
+  }
+  int ensure_published() {
+    if (published) return 0;
+    int r = publish();
+    if (r) return r;
+    HIPCHK(hipStreamSynchronize(stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
+    last_publish_ms = ms;
+    return 0;
+  }
+  int scratch(u64 bytes) {
+    if (bytes <= qbuf_bytes) return 0;
+    if (qbuf) (void)hipFree(qbuf);
+    qbuf = nullptr;
+    HIPCHK(hipMalloc(&qbuf, bytes));
+    qbuf_bytes = bytes;
+    return 0;
+  }
+};
+
+static bool valid(const crdt_engine* e) { return e && e->n_docs > 0; }
+
+extern "C" {
+
+int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
+  if (!cfg || !out || (cfg->leaf_cap != 32 && cfg->leaf_cap != 4)) return CRDT_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= cfg->device || cfg->device < 0) return CRDT_E_DEVICE;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return CRDT_E_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return CRDT_E_DEVICE;
+  std::unique_ptr<crdt_engine> e(new crdt_engine());
+  e->L = cfg->leaf_cap;
+  e->device = cfg->device;
+  if (hipSetDevice(e->device) != hipSuccess) return CRDT_E_DEVICE;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return CRDT_E_DEVICE;
+  for (auto& x : e->ev)
+    if (hipEventCreate(&x) != hipSuccess) return CRDT_E_DEVICE;
+  *out = e.release();
+  return 0;
+}
+
+void crdt_engine_destroy(crdt_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  e->release();
+  for (auto& x : e->ev)
+    if (x) (void)hipEventDestroy(x);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int crdt_docs_alloc(crdt_engine* e, uint64_t n) {
+  if (!e || n == 0 || n > 0xFFFFFFFFull) return CRDT_E_ARG;
+  return e->alloc_docs(n);
+}
+uint64_t crdt_num_docs(const crdt_engine* e) { return e ? e->n_docs : 0; }
+
+int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const char* const* names, uint16_t* out) {
+  if (!valid(e) || (n && (!doc || !names || !out))) return CRDT_E_ARG;
+  for (uint64_t i = 0; i < n; i++) {
+    if (doc[i] >= e->n_docs) return CRDT_E_ARG;
+    out[i] = (uint16_t)e->docs[doc[i]].agents.get_or_create(names[i]);
+  }
+  return 0;
+}
+
+static int stage_local_impl(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
+                            const crdt_local_txn* txns, const crdt_local_op* ops) {
+  if (!valid(e) || !docs || !txn_off || (!txns && txn_off[n_docs]) ) return CRDT_E_ARG;
+  std::vector<u64> ids(n_docs);
+  std::vector<std::vector<Rec>> streams(n_docs);
+  std::vector<StreamNeeds> needs(n_docs);
+  std::vector<const std::vector<Rec>*> sp(n_docs);
+  for (uint64_t i = 0; i < n_docs; i++) sp[i] = &streams[i];
+  // op offsets: ops are concatenated in txn order over all docs
+  u64 op = 0;
+  for (u64 t = 0; t < txn_off[0]; t++) op += txns[t].n_ops;
+  for (uint64_t i = 0; i < n_docs; i++) {
+    if (docs[i] >= e->n_docs) return CRDT_E_ARG;
+    ids[i] = docs[i];
+    for (u64 t = txn_off[i]; t < txn_off[i + 1]; t++) {
+      encode_local_txn(streams[i], needs[i], txns[t].agent, (const u32*)(ops + op), txns[t].n_ops);
+      op += txns[t].n_ops;
+    }
+  }
+  return e->stage(ids, sp, needs);
+}
+
+int crdt_stage_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
+                     const crdt_local_txn* txns, const crdt_local_op* ops) {
+  return stage_local_impl(e, n_docs, docs, txn_off, txns, ops);
+}
+
+int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint8_t* const* wire,
+                           const uint64_t* wire_len) {
+  if (!valid(e) || !docs || !wire || !wire_len) return CRDT_E_ARG;
+  std::vector<u64> ids(n_docs);
+  std::vector<std::vector<Rec>> streams(n_docs);
+  std::vector<StreamNeeds> needs(n_docs);
+  std::vector<const std::vector<Rec>*> sp(n_docs);
+  for (uint64_t i = 0; i < n_docs; i++) {
+    if (docs[i] >= e->n_docs) return CRDT_E_ARG;
+    ids[i] = docs[i];
+    WireView wv;
+    if (!wv.parse(wire[i], wire_len[i])) return CRDT_E_WIRE;
+    encode_remote(streams[i], needs[i], e->docs[docs[i]].agents, wv);
+    sp[i] = &streams[i];
+  }
+  return e->stage(ids, sp, needs);
+}
+
+int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t wire_len, uint32_t rename_idx,
+                                 const char* const* names) {
+  if (!valid(e) || !wire) return CRDT_E_ARG;
+  WireView wv;
+  if (!wv.parse(wire, wire_len)) return CRDT_E_WIRE;
+  // Every document gets its own interned names; documents whose name->agent-id mapping equals
+  // the first document's share one host-encoded stream (device copies are still per document).
+  std::vector<u64> ids(e->n_docs);
+  std::vector<std::vector<Rec>> uniq;
+  std::vector<const std::vector<Rec>*> sp(e->n_docs);
+  std::vector<StreamNeeds> needs(e->n_docs);
+  uniq.reserve(e->n_docs);
+  std::vector<u32> first_map;
+  for (u64 d = 0; d < e->n_docs; d++) {
+    ids[d] = d;
+    WireView w2 = wv;
+    if (names && rename_idx < w2.names.size()) w2.names[rename_idx] = names[d];
+    AgentTable& at = e->docs[d].agents;
+    std::vector<Rec> tmp;
+    bool fresh = at.names.empty();
+    if (d > 0 && fresh && !uniq.empty()) {
+      // intern in txn order (authors create, others look up) exactly as encode_remote does
+      AgentTable probe = at;
+      for (const auto& t : w2.txns) probe.get_or_create(w2.names[t.agent_name]);
+      std::vector<u32> m;
+      for (const auto& n : w2.names) m.push_back(probe.lookup(n));
+      if (m == first_map) {
+        at = probe;
+        sp[d] = &uniq[0];
+        needs[d] = needs[0];
+        continue;
+      }
+    }
+    uniq.emplace_back();
+    encode_remote(uniq.back(), needs[d], at, w2);
+    sp[d] = &uniq.back();
+    if (d == 0) for (const auto& n : w2.names) first_map.push_back(at.lookup(n));
+  }
+  return e->stage(ids, sp, needs);
+}
+
+int crdt_reset_async(crdt_engine* e) {
+  if (!valid(e)) return CRDT_E_ARG;
+  int r = e->set_device();
+  if (r) return r;
+  hipLaunchKernelGGL(k_reset_recpos, dim3((u32)((e->n_docs + 255) / 256)), dim3(256), 0, e->stream, e->st, (u32)e->n_docs, 0u);
+  return e->init_all();
+}
+
+int crdt_run(crdt_engine* e, int32_t* doc_status) {
+  if (!valid(e)) return CRDT_E_ARG;
+  return e->run(doc_status);
+}
+
+int crdt_run_async(crdt_engine* e) {
+  if (!valid(e)) return CRDT_E_ARG;
+  int r = e->set_device();
+  if (r) return r;
+  return e->launch_replay();
+}
+
+int crdt_publish_async(crdt_engine* e) {
+  if (!valid(e)) return CRDT_E_ARG;
+  return e->publish();
+}
+
+int crdt_sync(crdt_engine* e) {
+  if (!e) return CRDT_E_ARG;
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int crdt_apply_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
+                     const crdt_local_txn* txns, const crdt_local_op* ops, int32_t* doc_status) {
+  int r = stage_local_impl(e, n_docs, docs, txn_off, txns, ops);
+  if (r) return r;
+  std::vector<int32_t> all(e->n_docs);
+  r = e->run(all.data());
+  if (r) return r;
+  if (doc_status)
+    for (uint64_t i = 0; i < n_docs; i++) doc_status[i] = all[docs[i]];
+  return 0;
+}
+
+int crdt_apply_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint8_t* const* wire,
+                           const uint64_t* wire_len, int32_t* doc_status) {
+  int r = crdt_stage_remote_wire(e, n_docs, docs, wire, wire_len);
+  if (r) return r;
+  std::vector<int32_t> all(e->n_docs);
+  r = e->run(all.data());
+  if (r) return r;
+  if (doc_status)
+    for (uint64_t i = 0; i < n_docs; i++) doc_status[i] = all[docs[i]];
+  return 0;
+}
+
+int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint32_t* pos, uint16_t* agent, uint32_t* seq) {
+  if (!valid(e)) return CRDT_E_ARG;
+  if (!e->published) {
+    int r = e->publish();
+    if (r) return r;
+  }
+  if (!n) return 0;
+  u32 blocks = (u32)std::min<u64>((n + 255) / 256, 8192);
+  if (e->L == 32) hipLaunchKernelGGL(k_pos_to_loc<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+  else hipLaunchKernelGGL(k_pos_to_loc<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint16_t* agent, const uint32_t* seq, uint32_t* pos, uint8_t* deleted) {
+  if (!valid(e)) return CRDT_E_ARG;
+  if (!e->published) {
+    int r = e->publish();
+    if (r) return r;
+  }
+  if (!n) return 0;
+  u32 blocks = (u32)std::min<u64>((n + 255) / 256, 8192);
+  if (e->L == 32) hipLaunchKernelGGL(k_loc_to_pos<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
+  else hipLaunchKernelGGL(k_loc_to_pos<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int crdt_pos_to_loc(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint32_t* pos, uint16_t* agent, uint32_t* seq) {
+  if (!valid(e) || (n && (!doc || !pos || !agent || !seq))) return CRDT_E_ARG;
+  if (!n) return 0;
+  int r = e->ensure_published();
+  if (r) return r;
+  u64 bytes = n * (4 + 4 + 2 + 4) + 64;
+  r = e->scratch(bytes);
+  if (r) return r;
+  char* b = (char*)e->qbuf;
+  u32* d_doc = (u32*)b;
+  u32* d_pos = d_doc + n;
+  u32* d_seq = d_pos + n;
+  u16* d_ag = (u16*)(d_seq + n);
+  HIPCHK(hipMemcpyAsync(d_doc, doc, n * 4, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(d_pos, pos, n * 4, hipMemcpyHostToDevice, e->stream));
+  r = crdt_pos_to_loc_dev_async(e, n, d_doc, d_pos, d_ag, d_seq);
+  if (r) return r;
+  HIPCHK(hipMemcpyAsync(agent, d_ag, n * 2, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(seq, d_seq, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int crdt_loc_to_pos(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint16_t* agent, const uint32_t* seq, uint32_t* pos, uint8_t* deleted) {
+  if (!valid(e) || (n && (!doc || !agent || !seq || !pos || !deleted))) return CRDT_E_ARG;
+  if (!n) return 0;
+  int r = e->ensure_published();
+  if (r) return r;
+  u64 bytes = n * (4 + 4 + 4 + 2 + 1) + 64;
+  r = e->scratch(bytes);
+  if (r) return r;
+  char* b = (char*)e->qbuf;
+  u32* d_doc = (u32*)b;
+  u32* d_seq = d_doc + n;
+  u32* d_pos = d_seq + n;
+  u16* d_ag = (u16*)(d_pos + n);
+  u8* d_del = (u8*)(d_ag + n);
+  HIPCHK(hipMemcpyAsync(d_doc, doc, n * 4, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(d_seq, seq, n * 4, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(d_ag, agent, n * 2, hipMemcpyHostToDevice, e->stream));
+  r = crdt_loc_to_pos_dev_async(e, n, d_doc, d_ag, d_seq, d_pos, d_del);
+  if (r) return r;
+  HIPCHK(hipMemcpyAsync(pos, d_pos, n * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(deleted, d_del, n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int crdt_doc_len(crdt_engine* e, uint64_t n, const uint32_t* doc, uint32_t* len) {
+  if (!valid(e) || (n && (!doc || !len))) return CRDT_E_ARG;
+  int r = e->pull_states();
+  if (r) return r;
+  for (uint64_t i = 0; i < n; i++) {
+    if (doc[i] >= e->n_docs) return CRDT_E_ARG;
+    len[i] = e->st_h[doc[i]].len;
+  }
+  return 0;
+}
+
+int crdt_doc_status(crdt_engine* e, int32_t* status) {
+  if (!valid(e) || !status) return CRDT_E_ARG;
+  int r = e->pull_states();
+  if (r) return r;
+  for (u64 d = 0; d < e->n_docs; d++) status[d] = e->st_h[d].status == ST_NEED_CAPACITY ? ST_CAPACITY : e->st_h[d].status;
+  return 0;
+}
+
+int crdt_digest(crdt_engine* e, uint64_t* per_doc) {
+  if (!valid(e) || !per_doc) return CRDT_E_ARG;
+  int r = e->ensure_published();
+  if (r) return r;
+  HIPCHK(hipMemcpyAsync(per_doc, e->digest, e->n_docs * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+// Export: walk the document's directory on the host from device copies.
+int crdt_export_sizes(crdt_engine* e, uint32_t doc, uint64_t* s) {
+  if (!valid(e) || doc >= e->n_docs || !s) return CRDT_E_ARG;
+  int r = e->ensure_published();
+  if (r) return r;
+  r = e->pull_states();
+  if (r) return r;
+  const DocState& st = e->st_h[doc];
+  u32 cn = 0;
+  HIPCHK(hipMemcpy(&cn, e->canon_n + doc, 4, hipMemcpyDeviceToHost));
+  s[0] = st.n_entries; s[1] = st.n_leaves; s[2] = cn; s[3] = st.n_cwo; s[4] = st.n_del; s[5] = st.n_dd;
+  s[6] = st.n_txn; s[7] = st.n_par; s[8] = st.n_fr; s[9] = st.n_agents; s[10] = st.next_order; s[11] = st.len;
+  return 0;
+}
+
+int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_sizes, uint32_t* canon4, uint32_t* cwo4,
+                uint32_t* del3, uint32_t* dd3, uint32_t* txn5, uint32_t* parents, uint32_t* frontier) {
+  uint64_t s[12];
+  int r = crdt_export_sizes(e, doc, s);
+  if (r) return r;
+  const DocState& st = e->st_h[doc];
+  const DocSeg& sg = e->seg_h[doc];
+  u32 L = e->L;
+  if (raw4 || leaf_sizes) {
+    std::vector<GroupRec> groups(st.ng);
+    HIPCHK(hipMemcpy(groups.data(), e->groups + sg.grp_base, st.ng * sizeof(GroupRec), hipMemcpyDeviceToHost));
+    std::vector<u32> dl((size_t)st.n_blocks * GROUP);
+    HIPCHK(hipMemcpy(dl.data(), e->pools.dir_leaf + sg.blk_base * GROUP, dl.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<Span> lv((size_t)st.n_leaves * L);
+    HIPCHK(hipMemcpy(lv.data(), e->pools.leaves + sg.leaf_base * L, lv.size() * sizeof(Span), hipMemcpyDeviceToHost));
+    u64 k = 0, li = 0;
+    for (u32 g = 0; g < st.ng; g++)
+      for (u32 i = 0; i < groups[g].cnt; i++) {
+        u32 leaf = dl[(size_t)groups[g].blk * GROUP + i];
+        u32 n = 0;
+        for (u32 j = 0; j < L; j++) {
+          const Span& sp = lv[(size_t)leaf * L + j];
+          if (sp.len == 0) continue;
+          if (raw4) std::memcpy(raw4 + 4 * k, &sp, 16);
+          k++;
+          n++;
+        }
+        if (leaf_sizes) leaf_sizes[li] = n;
+        li++;
+      }
+  }
+  if (canon4 && s[2]) HIPCHK(hipMemcpy(canon4, e->pools.canon + sg.leaf_base * L, s[2] * 16, hipMemcpyDeviceToHost));
+  if (cwo4 && st.n_cwo) HIPCHK(hipMemcpy(cwo4, e->pools.cwo + sg.cwo_base, st.n_cwo * 16, hipMemcpyDeviceToHost));
+  if (del3 && st.n_del) HIPCHK(hipMemcpy(del3, e->pools.dels + sg.del_base, st.n_del * 12, hipMemcpyDeviceToHost));
+  if (dd3 && st.n_dd) HIPCHK(hipMemcpy(dd3, e->pools.dd + sg.dd_base, st.n_dd * 12, hipMemcpyDeviceToHost));
+  if (txn5 && st.n_txn) {
+    std::vector<TxnRec> t(st.n_txn);
+    HIPCHK(hipMemcpy(t.data(), e->pools.txns + sg.txn_base, st.n_txn * sizeof(TxnRec), hipMemcpyDeviceToHost));
+    for (u32 i = 0; i < st.n_txn; i++) {
+      txn5[5 * i] = t[i].order; txn5[5 * i + 1] = t[i].len; txn5[5 * i + 2] = t[i].shadow;
+      txn5[5 * i + 3] = t[i].poff; txn5[5 * i + 4] = t[i].pn;
+    }
+  }
+  if (parents && st.n_par) HIPCHK(hipMemcpy(parents, e->pools.parents + sg.par_base, st.n_par * 4, hipMemcpyDeviceToHost));
+  if (frontier && st.n_fr) HIPCHK(hipMemcpy(frontier, e->frontier + sg.fr_base, st.n_fr * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms) {
+  if (!e) return CRDT_E_ARG;
+  if (replay_ms) *replay_ms = e->last_replay_ms;
+  if (publish_ms) *publish_ms = e->last_publish_ms;
+  return 0;
+}
+
+void* crdt_stream(crdt_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+const char* crdt_last_error(void) { return g_last_error.c_str(); }
+
+}  // extern "C"

@@ -181,14 +181,16 @@ inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_
   if (c.leaf > MAX_LEAVES) c.leaf = MAX_LEAVES;
   c.blk = c.leaf / 32 + 2;
   c.map = track ? (u32)std::min<u64>(nd.orders + 1, 0xFFFFFFFFull) : 0;
-  c.cwo = (u32)nd.n_txn + 1;
-  c.txn = (u32)nd.n_txn + 1;
+  // RLE tables usually coalesce far below one run per txn; start small and grow on demand
+  // (ST_NEED_CAPACITY is resumable), exact bounds otherwise.
+  c.cwo = (u32)std::min<u64>(nd.n_txn + 1, 256 + nd.n_txn / 64);
+  c.txn = c.cwo;
   u64 arun = 0;
   for (u32 a = 0; a < n_agents; a++) arun += (a < nd.txns_per_agent.size() ? nd.txns_per_agent[a] : 0) + 1;
   c.arun = (u32)arun;
   c.del = (u32)std::min<u64>(nd.local_del + nd.remote_del_ops + 1, 0xFFFFFFFFull);
   c.dd = (u32)std::min<u64>(4 * nd.remote_del_ops + 64, 1u << 24);
-  c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + FRONTIER_CAP + 1, 0xFFFFFFFFull);
+  c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + FRONTIER_CAP + 1, 1024 + (nd.remote_parents + nd.n_txn) / 64);
   c.agent = n_agents;
   return c;
 }

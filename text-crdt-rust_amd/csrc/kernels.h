@@ -1,0 +1,280 @@
+// Device kernels of the engine.
+//   k_init      ListCRDT::new() per document (wave per document)
+//   k_replay    apply the staged record stream (wave per document, replay_core.h)
+//   k_relayout  move every document's state into re-sized pools (block per document)
+//   k_publish   flat index build: canonical spans (can_append compaction of the leaf entries in
+//               document order), visible-prefix vpos, order->span scatter, digest
+//   k_pos_to_loc / k_loc_to_pos   batched lookups on the published index (thread per query)
+#pragma once
+#include "replay_core.h"
+#include "wave_gpu.h"
+
+namespace crdt {
+
+struct PubOut {
+  Span* canon;    // [leaf_base*L + k]
+  u32* vpos;      // [leaf_base*L + k]  visible items before canonical span k
+  u32* span_of;   // [map_base + order]  canonical span containing item `order` (INVALID: delete order)
+  u32* canon_n;   // [doc]
+  u32* len;       // [doc]
+  u64* digest;    // [doc]
+};
+
+#define WAVES_PER_BLOCK 4
+
+template <int L>
+__global__ __launch_bounds__(256) void k_init(Pools P, u32 n) {
+  u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  if (d >= n) return;
+  WaveGPU<L> w;
+  Replayer<WaveGPU<L>, L> r(w, P, d);
+  r.init_empty();
+  for (u32 a = lane_id(); a < r.s.n_agents; a += 64) P.agents[r.seg.agent_base + a].run_cnt = 0;
+  r.finish();
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void k_replay(Pools P, u32 n) {
+  u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  if (d >= n) return;
+  WaveGPU<L> w;
+  Replayer<WaveGPU<L>, L> r(w, P, d);
+  if (r.s.status == ST_NEED_CAPACITY) r.s.status = ST_OK;  // resume after growth
+  if (r.s.status != ST_OK || r.s.rec_pos >= r.seg.rec_n) {
+    w.st((u32*)&P.st[d].status, (u32)r.s.status);
+    return;
+  }
+  r.begin();
+  r.run();
+  r.finish();
+}
+
+// Reset the per-call record cursor of every document (new stream staged).
+__global__ void k_reset_recpos(DocState* st, u32 n, u32 n_agents_dummy) {
+  u32 d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d < n) st[d].rec_pos = 0;
+}
+
+template <class T>
+__device__ __forceinline__ void bcopy(T* dst, const T* src, u64 n) {
+  for (u64 k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
+}
+
+// Move document state between pool sets (growth / re-staging).  src.st == dst.st.
+template <int L>
+__global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const DocSeg* old_seg, const u32* new_n_agents, u32 n) {
+  u32 d = blockIdx.x;
+  if (d >= n) return;
+  DocState s = dst.st[d];
+  DocSeg o = old_seg[d];
+  DocSeg w = dst.seg[d];
+  bcopy(dst.leaves + w.leaf_base * L, src.leaves + o.leaf_base * L, (u64)s.n_leaves * L);
+  bcopy(dst.slot_of_leaf + w.leaf_base, src.slot_of_leaf + o.leaf_base, s.n_leaves);
+  bcopy(dst.dir_leaf + w.blk_base * GROUP, src.dir_leaf + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
+  bcopy(dst.dir_vis + w.blk_base * GROUP, src.dir_vis + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
+  if (w.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);
+  bcopy(dst.cwo + w.cwo_base, src.cwo + o.cwo_base, s.n_cwo);
+  bcopy(dst.dels + w.del_base, src.dels + o.del_base, s.n_del);
+  bcopy(dst.dd + w.dd_base, src.dd + o.dd_base, s.n_dd);
+  bcopy(dst.txns + w.txn_base, src.txns + o.txn_base, s.n_txn);
+  bcopy(dst.parents + w.par_base, src.parents + o.par_base, s.n_par);
+  for (u32 a = 0; a < s.n_agents; a++) {
+    AgentRec ao = src.agents[o.agent_base + a];
+    AgentRec an = dst.agents[w.agent_base + a];
+    bcopy(dst.arun + w.arun_base + an.run_base, src.arun + o.arun_base + ao.run_base, ao.run_cnt);
+    __syncthreads();
+    if (threadIdx.x == 0) dst.agents[w.agent_base + a].run_cnt = ao.run_cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) dst.st[d].n_agents = new_n_agents[d];
+}
+
+// ---------------------------------------------------------------------------------------------
+// digest helpers (identical to oracle/crdt_oracle.hpp)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ u64 mix64(u64 z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ u64 elem_hash(u32 section, u64 idx, u64 a, u64 b) {
+  u64 k = mix64(((u64)section << 56) ^ idx);
+  return mix64(mix64(k ^ a) ^ b);
+}
+__device__ __forceinline__ u64 wave_sum64(u64 v) {
+  for (u32 off = 32; off >= 1; off >>= 1) {
+    u32 lo = (u32)v, hi = (u32)(v >> 32);
+    u32 src = lane_id() ^ off;
+    u32 olo = shfl(lo, src), ohi = shfl(hi, src);
+    v += ((u64)ohi << 32) | olo;
+  }
+  return v;
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
+  u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  if (d >= n) return;
+  WaveGPU<L> w;
+  DocState s = w.ldT(P.st + d);
+  DocSeg seg = P.seg[d];
+  u32 l = lane_id();
+  if (s.status != ST_OK && s.status != ST_NEED_CAPACITY) {
+    if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
+    return;
+  }
+  Span* canon = O.canon + seg.leaf_base * L;
+  u32* vpos = O.vpos + seg.leaf_base * L;
+  w.root_load(P.groups + seg.grp_base, s.ng);
+  u32 out = 0, vis = 0;
+  bool have = false;
+  Span open{0, 0, 0, 0};
+  u32 open_vpos = 0;
+  for (u32 g = 0; g < s.ng; g++) {
+    u32 blk = w.root_blk(g), cnt = w.root_cnt(g);
+    const u32* dl = P.dir_leaf + (seg.blk_base + blk) * GROUP;
+    u32 mydl = l < cnt ? dl[l] : 0u;
+    for (u32 i = 0; i < cnt; i++) {
+      u32 leaf = rdlane(mydl, i);
+      u32 nn = w.cache_load(P.leaves + (seg.leaf_base + leaf) * L);
+      for (u32 j = 0; j < nn; j++) {
+        Span sp = w.cget(j);
+        if (have && can_append(open, sp)) {
+          open.len += sp.len;
+        } else {
+          if (have) {
+            if (l == 0) { canon[out] = open; vpos[out] = open_vpos; }
+            out++;
+          }
+          open = sp;
+          open_vpos = vis;
+          have = true;
+        }
+        vis += clen(sp);
+      }
+    }
+  }
+  if (have) {
+    if (l == 0) { canon[out] = open; vpos[out] = open_vpos; }
+    out++;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // order -> canonical span scatter (delete orders stay INVALID)
+  u32* so = O.span_of + seg.map_base;
+  w.fill(so, s.next_order, INVALID);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  u64 h = 0;
+  for (u32 k = l; k < out; k += 64) {
+    Span sp = canon[k];
+    u32 ln = slen(sp);
+    for (u32 t = 0; t < ln; t++) so[sp.order + t] = k;
+    h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
+  }
+  const CwoRun* cwo = P.cwo + seg.cwo_base;
+  for (u32 k = l; k < s.n_cwo; k += 64) {
+    CwoRun r = cwo[k];
+    h += elem_hash(2, k, ((u64)r.key << 32) | r.agent, ((u64)r.seq << 32) | r.len);
+  }
+  const DelRun* dels = P.dels + seg.del_base;
+  for (u32 k = l; k < s.n_del; k += 64) {
+    DelRun r = dels[k];
+    h += elem_hash(3, k, ((u64)r.key << 32) | r.order, r.len);
+  }
+  const DDRun* dd = P.dd + seg.dd_base;
+  for (u32 k = l; k < s.n_dd; k += 64) {
+    DDRun r = dd[k];
+    h += elem_hash(4, k, ((u64)r.key << 32) | r.len, r.excess);
+  }
+  const TxnRec* tx = P.txns + seg.txn_base;
+  const u32* par = P.parents + seg.par_base;
+  for (u32 k = l; k < s.n_txn; k += 64) {
+    TxnRec t = tx[k];
+    h += elem_hash(5, k, ((u64)t.order << 32) | t.len, ((u64)t.shadow << 32) | t.pn);
+    for (u32 j = 0; j < t.pn; j++) h += elem_hash(6, t.poff + j, par[t.poff + j], k);
+  }
+  const u32* fr = P.frontier + seg.fr_base;
+  for (u32 k = l; k < s.n_fr; k += 64) h += elem_hash(7, k, fr[k], 0);
+  h = wave_sum64(h);
+  u64 counts = elem_hash(8, 0, ((u64)s.len << 32) | out, ((u64)s.n_cwo << 32) | s.n_del);
+  counts ^= elem_hash(9, 0, ((u64)s.n_dd << 32) | s.n_txn, ((u64)s.n_fr << 32) | s.n_par);
+  if (l == 0) {
+    O.canon_n[d] = out;
+    O.len[d] = s.len;
+    O.digest[d] = mix64(h ^ counts);
+  }
+}
+
+template <class T>
+__device__ __forceinline__ i32 find_run(const T* b, u32 n, u32 x) {  // simple_rle.rs:18-25 search
+  u32 lo = 0, hi = n;
+  while (lo < hi) {
+    u32 mid = (lo + hi) >> 1;
+    u32 k = ((const u32*)&b[mid])[0];
+    u32 ln = WaveGPU<32>::rlen(b[mid]);
+    if (x < k) hi = mid;
+    else if (x >= k + ln) lo = mid + 1;
+    else return (i32)mid;
+  }
+  return -1;
+}
+
+template <int L>
+__global__ void k_pos_to_loc(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* doc, const u32* pos, u16* agent, u32* seq) {
+  for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (u64)gridDim.x * blockDim.x) {
+    u32 d = doc[q], p = pos[q];
+    u16 a = 0xFFFF;
+    u32 sq = INVALID;
+    if (d < n_docs) {
+      i32 stt = P.st[d].status;
+      if ((stt == ST_OK || stt == ST_NEED_CAPACITY) && p < O.len[d]) {
+        DocSeg seg = P.seg[d];
+        const u32* vp = O.vpos + seg.leaf_base * L;
+        const Span* cn = O.canon + seg.leaf_base * L;
+        u32 lo = 0, hi = O.canon_n[d];
+        while (lo < hi) {
+          u32 mid = (lo + hi) >> 1;
+          if (vp[mid] <= p) lo = mid + 1; else hi = mid;
+        }
+        u32 k = lo - 1;
+        u32 order = cn[k].order + (p - vp[k]);
+        const CwoRun* cw = P.cwo + seg.cwo_base;
+        i32 r = find_run(cw, P.st[d].n_cwo, order);
+        if (r >= 0) { a = (u16)cw[r].agent; sq = cw[r].seq + (order - cw[r].key); }
+      }
+    }
+    agent[q] = a;
+    seq[q] = sq;
+  }
+}
+
+template <int L>
+__global__ void k_loc_to_pos(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* doc, const u16* agent, const u32* seq, u32* pos, u8* deleted) {
+  for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (u64)gridDim.x * blockDim.x) {
+    u32 d = doc[q];
+    u32 ps = INVALID;
+    u8 dl = 2;
+    if (d < n_docs) {
+      DocState s = P.st[d];
+      if ((s.status == ST_OK || s.status == ST_NEED_CAPACITY) && agent[q] < s.n_agents) {
+        DocSeg seg = P.seg[d];
+        AgentRec A = P.agents[seg.agent_base + agent[q]];
+        const ARun* ar = P.arun + seg.arun_base + A.run_base;
+        i32 r = find_run(ar, A.run_cnt, seq[q]);
+        if (r >= 0) {
+          u32 order = ar[r].order + (seq[q] - ar[r].key);
+          u32 k = O.span_of[seg.map_base + order];
+          if (k != INVALID) {
+            Span sp = O.canon[seg.leaf_base * L + k];
+            ps = O.vpos[seg.leaf_base * L + k] + (sp.len > 0 ? order - sp.order : 0u);
+            dl = sp.len < 0 ? 1 : 0;
+          }
+        }
+      }
+    }
+    pos[q] = ps;
+    deleted[q] = dl;
+  }
+}
+
+}  // namespace crdt

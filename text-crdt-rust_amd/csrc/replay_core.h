@@ -71,6 +71,8 @@ struct Replayer {
     s.n_cwo = s.n_del = s.n_dd = s.n_txn = s.n_par = 0;
     s.n_fr = 1;
     s.n_items = 0;
+    s.cap_need = 0;
+    s.n_entries = 0;
     w.zero_leaf(leafptr(0), L);
     w.st(dleaf(0), 0u);
     w.st(dvis(0), 0u);
@@ -346,6 +348,7 @@ struct Replayer {
     }
     u32 space = nitems + (has_rem ? 1u : 0u);
     if (space > (u32)L / 2) return false;  // mutations.rs:121 assert
+    s.n_entries += space;
     bool rem_moved = false;
     if (c_n + space > (u32)L) {
       if (c.idx < (u32)L / 2) {

@@ -47,19 +47,19 @@ struct WaveGPU {
 
   // ---- scalar memory helpers (every lane touches the same address: uniform results, and a
   //      store is then visible to every lane's later loads by per-thread program order)
-  __device__ __forceinline__ u32 ld(const u32* p) const { return uni(*(volatile const u32*)p); }
-  __device__ __forceinline__ void st(u32* p, u32 v) const { *(volatile u32*)p = v; }
-  __device__ __forceinline__ void st(i32* p, i32 v) const { *(volatile i32*)p = v; }
+  __device__ __forceinline__ u32 ld(const u32* p) const { return uni(*(const u32*)p); }
+  __device__ __forceinline__ void st(u32* p, u32 v) const { *(u32*)p = v; }
+  __device__ __forceinline__ void st(i32* p, i32 v) const { *(i32*)p = v; }
   template <class T> __device__ __forceinline__ T ldT(const T* p) const {
     T t;
-    const volatile u32* s = (const volatile u32*)p;
+    const u32* s = (const u32*)p;
     u32* o = (u32*)&t;
 #pragma unroll
     for (u32 k = 0; k < sizeof(T) / 4; k++) o[k] = uni(s[k]);
     return t;
   }
   template <class T> __device__ __forceinline__ void stT(T* p, const T& v) const {
-    volatile u32* s = (volatile u32*)p;
+    u32* s = (u32*)p;
     const u32* o = (const u32*)&v;
 #pragma unroll
     for (u32 k = 0; k < sizeof(T) / 4; k++) s[k] = o[k];
@@ -99,7 +99,7 @@ struct WaveGPU {
     while (hi - lo > 64) {
       u32 step = (hi - lo + 63) / 64;
       u32 idx = lo + l * step;
-      bool ok = idx < hi && *(const volatile u32*)&base[idx] <= needle;  // key is the first field
+      bool ok = idx < hi && *(const u32*)&base[idx] <= needle;  // key is the first field
       u64 m = ballot(ok);
       if (m == 0) return -1;
       u32 t = 63 - __builtin_clzll(m);
@@ -108,7 +108,7 @@ struct WaveGPU {
       hi = nh < hi ? nh : hi;
     }
     u32 idx = lo + l;
-    bool ok = idx < hi && *(const volatile u32*)&base[idx] <= needle;
+    bool ok = idx < hi && *(const u32*)&base[idx] <= needle;
     u64 m = ballot(ok);
     if (m == 0) return -1;
     u32 k = lo + (63 - __builtin_clzll(m));
@@ -130,14 +130,14 @@ struct WaveGPU {
   __device__ __forceinline__ u32 cache_load(const Span* p) {
     u32 l = lane_id();
     if (l < (u32)L) {
-      uint4 v = *(const volatile uint4*)(p + l);
+      uint4 v = *(const uint4*)(p + l);
       eo = v.x; el = v.y; er = v.z; en = (i32)v.w;
     } else { eo = el = er = 0; en = 0; }
     return __popcll(ballot(l < (u32)L && en != 0));
   }
   __device__ __forceinline__ void cache_store(Span* p, u32 /*n*/) const {
     u32 l = lane_id();
-    if (l < (u32)L) *(volatile uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
+    if (l < (u32)L) *(uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
   }
   __device__ __forceinline__ Span cget(u32 i) const {
     return Span{rdlane(eo, i), rdlane(el, i), rdlane(er, i), (i32)rdlane((u32)en, i)};
@@ -177,7 +177,7 @@ struct WaveGPU {
     u32 src = l + idx - padding;  // valid only when l >= padding
     u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
     bool take = l >= padding && src < n;
-    if (l < (u32)L) *(volatile uint4*)(dst + l) = take ? make_uint4(o, a, b, c) : make_uint4(0, 0, 0, 0);
+    if (l < (u32)L) *(uint4*)(dst + l) = take ? make_uint4(o, a, b, c) : make_uint4(0, 0, 0, 0);
   }
   __device__ __forceinline__ void cache_clear(u32 a, u32 b) {
     u32 l = lane_id();
@@ -201,7 +201,7 @@ struct WaveGPU {
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       u32 i = r * 64 + l;
       u32 b = 0, c = 0, v = 0;
-      if (i < ng) { uint4 x = *(const volatile uint4*)(g + i); b = x.x; c = x.y; v = x.z; }
+      if (i < ng) { uint4 x = *(const uint4*)(g + i); b = x.x; c = x.y; v = x.z; }
       gb.put(r, b); gc.put(r, c); gv.put(r, v);
     }
   }
@@ -210,7 +210,7 @@ struct WaveGPU {
 #pragma unroll
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       u32 i = r * 64 + l;
-      if (i < ng) *(volatile uint4*)(g + i) = make_uint4(gb.get(r), gc.get(r), gv.get(r), 0);
+      if (i < ng) *(uint4*)(g + i) = make_uint4(gb.get(r), gc.get(r), gv.get(r), 0);
     }
   }
   __device__ __forceinline__ u32 root_blk(u32 g) const { return rdlane(gb.get(g >> 6), g & 63); }
@@ -277,7 +277,7 @@ struct WaveGPU {
   // ---------------------------------------------------------------- directory blocks (HBM)
   __device__ __forceinline__ bool blk_find_pos(const u32* dv, u32 cnt, u32 rem, u32& i, u32& before) const {
     u32 l = lane_id();
-    u32 x = l < cnt ? *(const volatile u32*)(dv + l) : 0u;
+    u32 x = l < cnt ? *(const u32*)(dv + l) : 0u;
     u32 incl = wave_incl_scan(x);
     u32 k = __popcll(ballot(l < cnt && incl <= rem));
     if (k >= cnt) return false;
@@ -287,26 +287,26 @@ struct WaveGPU {
   }
   __device__ __forceinline__ void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
     u32 l = lane_id();
-    u32 ol = l < cnt ? *(volatile u32*)(dl + l) : 0u;
-    u32 ov = l < cnt ? *(volatile u32*)(dv + l) : 0u;
+    u32 ol = l < cnt ? *(u32*)(dl + l) : 0u;
+    u32 ov = l < cnt ? *(u32*)(dv + l) : 0u;
     u32 sl = shfl(ol, l - 1), sv = shfl(ov, l - 1);
     u32 nlf = l < i ? ol : (l == i ? leaf : sl);
     u32 nvs = l < i ? ov : (l == i ? vis : sv);
     if (l >= i && l <= cnt) {
-      *(volatile u32*)(dl + l) = nlf;
-      *(volatile u32*)(dv + l) = nvs;
-      *(volatile u32*)(sol + nlf) = (blk << 6) | l;
+      *(u32*)(dl + l) = nlf;
+      *(u32*)(dv + l) = nvs;
+      *(u32*)(sol + nlf) = (blk << 6) | l;
     }
   }
   __device__ __forceinline__ u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
     u32 l = lane_id();
     u32 lf = 0, v = 0;
     if (l >= 32) {
-      lf = *(const volatile u32*)(dl + l);
-      v = *(const volatile u32*)(dv + l);
-      *(volatile u32*)(ndl + l - 32) = lf;
-      *(volatile u32*)(ndv + l - 32) = v;
-      *(volatile u32*)(sol + lf) = (nb << 6) | (l - 32);
+      lf = *(const u32*)(dl + l);
+      v = *(const u32*)(dv + l);
+      *(u32*)(ndl + l - 32) = lf;
+      *(u32*)(ndv + l - 32) = v;
+      *(u32*)(sol + lf) = (nb << 6) | (l - 32);
     }
     return wave_sum(v);
   }
