@@ -34,6 +34,8 @@ struct WaveCPU {
   void st_txn(TxnRec* p, const TxnRec& v) const { *p = v; }
   Rec ld_rec(const Rec* p) const { return *p; }
   void st_state(DocState* p, const DocState& s) const { *p = s; }
+  DocState ld_state(const DocState* p) const { return *p; }
+  DocSeg ld_seg(const DocSeg* p) const { return *p; }
   void fill(u32* p, u32 n, u32 v) const { for (u32 k = 0; k < n; k++) p[k] = v; }
   void zero_leaf(Span* p, u32 n) const { std::memset(p, 0, sizeof(Span) * n); }
 

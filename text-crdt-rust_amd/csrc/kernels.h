@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void k_init(Pools P, u32 n) {
 
 template <int L>
 __global__ __launch_bounds__(256) void k_replay(Pools P, u32 n) {
-  u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
   if (d >= n) return;
   WaveGPU<L> w;
   Replayer<WaveGPU<L>, L> r(w, P, d);

@@ -47,8 +47,8 @@ struct Replayer {
   u32 c_vstart = 0;
 
   CRDT_HD Replayer(W& w_, const Pools& p, u32 doc) : w(w_), P(p), d(doc) {
-    seg = P.seg[d];
-    s = P.st[d];
+    seg = w.ld_seg(P.seg + d);
+    s = w.ld_state(P.st + d);
     track = (seg.flags & DOC_TRACK_MAP) != 0;
   }
 
@@ -292,10 +292,10 @@ struct Replayer {
     return nl;
   }
   // mutations.rs:17-179 insert_internal
-  CRDT_HD bool insert_internal(const Span* items0, u32 nitems, Cursor& c) {
+  // items are passed as three named values (n <= 3) so they stay in registers
+  CRDT_HD static Span pick(const Span& a, const Span& b, const Span& c, u32 k) { return k == 0 ? a : (k == 1 ? b : c); }
+  CRDT_HD bool insert_internal(Span i0, Span i1, Span i2, u32 nitems, Cursor& c) {
     if (nitems == 0) return true;
-    Span items[3];
-    for (u32 k = 0; k < nitems; k++) items[k] = items0[k];
     u32 ib = 0;  // items[ib .. ib+nitems)
     ensure(c.leaf);
     if (c.off == 0 && c.idx > 0) {
@@ -315,7 +315,7 @@ struct Replayer {
       Span cur = w.cget(c.idx);
       u32 it = 0;
       while (it < nitems) {
-        const Span& nx = items[ib + it];
+        Span nx = pick(i0, i1, i2, ib + it);
         if (!can_append(cur, nx)) break;
         notify(nx, c.leaf);
         cur.len += nx.len;
@@ -333,7 +333,7 @@ struct Replayer {
         Span nx2 = w.cget(c.idx);
         bool any = false;
         while (true) {
-          const Span& it2 = items[ib + end];
+          Span it2 = pick(i0, i1, i2, ib + end);
           if (!can_append(it2, nx2)) break;
           notify(it2, c.leaf);
           nx2.order = it2.order;  // prepend (span.rs:61-64): origin_left is NOT updated
@@ -369,22 +369,24 @@ struct Replayer {
       c_n += space;
     }
     for (u32 k = 0; k < nitems; k++) {
-      notify(items[ib + k], c.leaf);
-      set(c.idx + k, items[ib + k]);
+      Span x = pick(i0, i1, i2, ib + k);
+      notify(x, c.leaf);
+      set(c.idx + k, x);
     }
+    Span last = pick(i0, i1, i2, ib + nitems - 1);
     c.idx += nitems - 1;
-    c.off = slen(items[ib + nitems - 1]);
+    c.off = slen(last);
     if (has_rem) {
       if (rem_moved) notify(rem, c.leaf);
       set(c.idx + 1, rem);
     }
     return true;
   }
-  // mutations.rs:185-200
-  CRDT_HD bool replace_entry(Cursor& c, const Span* items, u32 n) {
-    set(c.idx, items[0]);
-    c.off = slen(items[0]);
-    return insert_internal(items + 1, n - 1, c);
+  // mutations.rs:185-200 (items = i0 then up to two more)
+  CRDT_HD bool replace_entry(Cursor& c, Span i0, Span i1, Span i2, u32 n) {
+    set(c.idx, i0);
+    c.off = slen(i0);
+    return insert_internal(i1, i2, i2, n - 1, c);
   }
   // mutations.rs:227-277.  del_next != nullptr: local delete, stream the deactivated run into
   // the delete log (extend_delete + Rle::append compose to the same list).
@@ -403,9 +405,9 @@ struct Replayer {
       *del_next += (u32)entry.len;
     }
     entry.len = -entry.len;
-    if (ha && hc) { Span it[3] = {a, entry, cc}; return replace_entry(c, it, 3); }
-    if (ha) { Span it[2] = {a, entry}; return replace_entry(c, it, 2); }
-    if (hc) { Span it[2] = {entry, cc}; return replace_entry(c, it, 2); }
+    if (ha && hc) return replace_entry(c, a, entry, cc, 3);
+    if (ha) return replace_entry(c, a, entry, entry, 2);
+    if (hc) return replace_entry(c, entry, cc, cc, 2);
     set(c.idx, entry);
     c.off = replaced;
     return true;
@@ -635,7 +637,7 @@ struct Replayer {
     }
     if (scanning) cursor = scan_start;
     // RangeTree::insert (mutations.rs:202-224)
-    if (!insert_internal(&item, 1, cursor)) return ST_INTERNAL;
+    if (!insert_internal(item, item, item, 1, cursor)) return ST_INTERNAL;
     s.n_items += (u32)item.len;
     return ST_OK;
   }

@@ -80,6 +80,8 @@ struct WaveGPU {
     return Rec{uni(v.x), uni(v.y), uni(v.z), uni(v.w)};
   }
   __device__ __forceinline__ void st_state(DocState* p, const DocState& s) const { stT(p, s); }
+  __device__ __forceinline__ DocState ld_state(const DocState* p) const { return ldT(p); }
+  __device__ __forceinline__ DocSeg ld_seg(const DocSeg* p) const { return ldT(p); }
 
   // lane-parallel fill of n u32
   __device__ __forceinline__ void fill(u32* p, u32 n, u32 v) const {
