@@ -1,0 +1,29 @@
+"""Profiling driver: stage `docs` copies of a trace's remote form and run ONE replay + publish."""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "text-crdt-rust_amd"))
+import crdt_amd  # noqa: E402
+from crdt_amd.traces import load_remote_wire, load_trace  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--docs", type=int, default=64)
+ap.add_argument("--trace", default="automerge-paper")
+ap.add_argument("--local", action="store_true")
+a = ap.parse_args()
+e = crdt_amd.Engine(a.docs, 32)
+if a.local:
+    t = load_trace(a.trace)
+    ag = e.agent_intern(list(range(a.docs)), ["jeremy"] * a.docs)
+    e.apply_trace(list(range(a.docs)), int(ag[0]), t.counts, t.patches, stage_only=True)
+else:
+    w = load_remote_wire(a.trace)
+    e.stage_remote_replicated(w, 0, ["u%05d" % i for i in range(a.docs)])
+t0 = time.time()
+st = e.run()
+e.publish_async()
+e.sync()
+print("status ok:", bool((st == 0).all()), "replay_ms", e.timings()[0], "wall", time.time() - t0)

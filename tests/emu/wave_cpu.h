@@ -93,7 +93,11 @@ struct WaveCPU {
   void cache_clear(u32 a, u32 b) { for (u32 i = a; i < b; i++) c[i] = Span{0, 0, 0, 0}; }
   void cache_shift_right(u32 idx, u32 n, u32 k) {
     for (i32 i = (i32)n - 1; i >= (i32)idx; i--) c[i + k] = c[i];
+    for (u32 i = idx; i < idx + k; i++) c[i] = Span{0, 0, 0, 0};
   }
+  Rec rb[64];
+  void rec_block_load(const Rec* p, u32 n) { for (u32 i = 0; i < n; i++) rb[i] = p[i]; }
+  Rec rec_get(u32 k) const { return rb[k]; }
 
   // directory root
   void root_init(u32 blk, u32 cnt, u32 vis) {
@@ -120,10 +124,10 @@ struct WaveCPU {
     }
     return false;
   }
-  bool blk_find_pos(const u32* dv, u32 cnt, u32 rem, u32& i, u32& before) const {
+  bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
     u32 acc = 0;
     for (u32 k = 0; k < cnt; k++) {
-      if (rem < acc + dv[k]) { i = k; before = acc; return true; }
+      if (rem < acc + dv[k]) { i = k; before = acc; leaf = dl[k]; return true; }
       acc += dv[k];
     }
     return false;

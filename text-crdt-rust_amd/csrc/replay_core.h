@@ -10,16 +10,18 @@
 //   * a two-level wave directory instead of internal nodes: 64-slot blocks (leaf id + visible
 //     count) in HBM and a root level of up to 256 groups held in VGPRs (lane = group), so every
 //     descent is two wave-wide scans and every leaf insertion one 64-lane shift;
-//   * a leaf cache in VGPRs (lane i = entry i) with write-back, so runs of local edits in one
-//     leaf never touch the directory;
+//   * a write-back leaf cache in VGPRs (lane i = entry i) that also remembers its directory slot
+//     and visible count, so runs of edits in one leaf touch neither HBM loads nor the directory;
 //   * an order->leaf table (u32 per order) replacing the SplitList, written only when a run
-//     changes leaf (the reference's notify() semantics).
+//     changes leaf (the reference's notify() semantics) and never read when the target item is
+//     in the cached leaf;
+//   * register-resident tails of every RLE table (client_with_order, the author's item_orders,
+//     deletes, txns, frontier) and a 64-record prefetch of the op stream, so the common op issues
+//     no dependent HBM load at all (stores are fire-and-forget).
 //
 // Control flow is wave-uniform; every lane-parallel step goes through the backend W:
 //   W = WaveGPU (wave_gpu.h, the product) or WaveCPU (tests/emu, a test-only emulation used to
 //   debug this file against the oracle without a GPU).
-//
-// Function-by-function correspondence is noted as `ref:` comments.
 #pragma once
 #include "crdt_types.h"
 
@@ -38,13 +40,28 @@ struct Replayer {
   DocState s;
   bool track;
 
-  // leaf cache (uniform bookkeeping; the entries live in W)
+  // ---- leaf cache bookkeeping (the entries themselves live in W)
   u32 c_leaf = INVALID;
   u32 c_n = 0;
   bool c_dirty = false;
-  u32 c_vis = 0;         // visible count of c_leaf as recorded in the directory
-  bool c_vs_ok = false;  // c_vstart valid
-  u32 c_vstart = 0;
+  u32 c_vis = 0;      // visible count of c_leaf as recorded in the directory
+  u32 c_now = 0;      // visible count of the cached entries right now
+  u32 c_blk = 0, c_i = 0;  // directory slot of c_leaf
+  bool c_vs_ok = false;
+  u32 c_vstart = 0;   // visible items before c_leaf (valid if c_vs_ok)
+
+  // ---- register-resident RLE tails (written through to HBM on every change)
+  CwoRun cwo_last{0, 0, 0, 0};
+  DelRun del_last{0, 0, 0};
+  TxnRec txn_last{0, 0, 0, 0, 0, {0, 0, 0}};
+  u32 txn_last_p0 = 0;
+  u32 fr0 = ROOT_ORDER;
+  u32 ag_id = INVALID;  // agent cache (the txn author)
+  AgentRec ag{0, 0, 0, 0};
+  ARun ag_last{0, 0, 0, 0};
+
+  // ---- record prefetch
+  u32 rb_base = 0x80000000u;  // pos - rb_base >= 64 for every valid pos
 
   CRDT_HD Replayer(W& w_, const Pools& p, u32 doc) : w(w_), P(p), d(doc) {
     seg = w.ld_seg(P.seg + d);
@@ -57,8 +74,10 @@ struct Replayer {
   CRDT_HD u32* dleaf(u32 blk) const { return P.dir_leaf + (seg.blk_base + blk) * (u64)GROUP; }
   CRDT_HD u32* dvis(u32 blk) const { return P.dir_vis + (seg.blk_base + blk) * (u64)GROUP; }
   CRDT_HD u32* sol() const { return P.slot_of_leaf + seg.leaf_base; }
+  CRDT_HD AgentRec* agp(u32 a) const { return P.agents + seg.agent_base + a; }
+  CRDT_HD ARun* arunp(const AgentRec& A) const { return P.arun + seg.arun_base + A.run_base; }
 
-  // ------------------------------------------------------------------ init / finish
+  // ------------------------------------------------------------------ init / begin / finish
   // New empty document: ListCRDT::new (doc.rs:51-64): one empty root leaf, frontier [ROOT].
   CRDT_HD void init_empty() {
     s.status = ST_OK;
@@ -80,15 +99,35 @@ struct Replayer {
     w.st(P.frontier + seg.fr_base, ROOT_ORDER);
     w.root_init(0u, 1u, 0u);
   }
-  CRDT_HD void begin() { w.root_load(P.groups + seg.grp_base, s.ng); }
+  CRDT_HD void begin() {
+    w.root_load(P.groups + seg.grp_base, s.ng);
+    if (s.n_cwo) cwo_last = w.ld_cwo(P.cwo + seg.cwo_base + s.n_cwo - 1);
+    if (s.n_del) del_last = w.ld_del(P.dels + seg.del_base + s.n_del - 1);
+    if (s.n_txn) {
+      txn_last = w.ld_txn(P.txns + seg.txn_base + s.n_txn - 1);
+      if (txn_last.pn) txn_last_p0 = w.ld(P.parents + seg.par_base + txn_last.poff);
+    }
+    fr0 = w.ld(P.frontier + seg.fr_base);
+  }
   CRDT_HD void finish() {
     commit();
     w.root_store(P.groups + seg.grp_base, s.ng);
     w.st_state(P.st + d, s);
   }
 
+  // ------------------------------------------------------------------ records
+  CRDT_HD Rec rec(u32 pos) {
+    if (pos - rb_base >= 64u) {
+      rb_base = pos;
+      u32 n = seg.rec_n - pos;
+      w.rec_block_load(P.recs + seg.rec_base + pos, n < 64u ? n : 64u);
+    }
+    return w.rec_get(pos - rb_base);
+  }
+
   // ------------------------------------------------------------------ directory
   CRDT_HD void slot_of(u32 leaf, u32& blk, u32& i) const {
+    if (leaf == c_leaf) { blk = c_blk; i = c_i; return; }
     u32 v = w.ld(sol() + leaf);
     blk = v >> 6;
     i = v & 63u;
@@ -111,19 +150,17 @@ struct Replayer {
     if (g + 1 < s.ng) return w.ld(dleaf(w.root_blk(g + 1)));
     return INVALID;
   }
-  CRDT_HD void dir_add_vis(u32 leaf, i64 delta) {
-    if (delta == 0) return;
-    u32 blk, i;
-    slot_of(leaf, blk, i);
-    u32* p = dvis(blk) + i;
-    w.st(p, (u32)((i64)w.ld(p) + delta));
-    w.root_add_vis(w.root_find_blk(s.ng, blk), (u32)delta);
-    s.len = (u32)((i64)s.len + delta);
+  // Record the cached leaf's new visible count in the directory.
+  CRDT_HD void dir_set_cached_vis(u32 v) {
+    if (v == c_vis) return;
+    w.st(dvis(c_blk) + c_i, v);
+    w.root_add_vis(w.root_find_blk(s.ng, c_blk), v - c_vis);
+    s.len += v - c_vis;
+    c_vis = v;
   }
-  // Insert leaf `nl` (visible count v) right after leaf `a` in document order.
-  CRDT_HD void dir_insert_after(u32 a, u32 nl, u32 v) {
-    u32 blk, i;
-    slot_of(a, blk, i);
+  // Insert leaf `nl` (visible count v) right after the cached leaf in document order.
+  CRDT_HD void dir_insert_after_cached(u32 nl, u32 v) {
+    u32 blk = c_blk, i = c_i;
     u32 g = w.root_find_blk(s.ng, blk);
     u32 cnt = w.root_cnt(g);
     if (cnt == GROUP) {  // split the block: [32, 64) -> new block in group g+1
@@ -132,7 +169,7 @@ struct Replayer {
       w.root_set(g, blk, 32u, w.root_vis(g) - mv);
       w.root_insert(s.ng, g + 1, nb, 32u, mv);
       s.ng++;
-      if (i >= 32) { blk = nb; i -= 32; g = g + 1; }
+      if (i >= 32) { blk = nb; i -= 32; g = g + 1; c_blk = nb; c_i = i; }
       cnt = 32;
     }
     w.blk_insert(dleaf(blk), dvis(blk), cnt, i + 1, nl, v, sol(), blk);
@@ -140,13 +177,12 @@ struct Replayer {
     s.len += v;
   }
   // First leaf whose visible range contains `pos` (root.rs:54-88 descent, ContentIndex).
-  CRDT_HD bool find_by_pos(u32 pos, u32& leaf, u32& vstart) const {
+  CRDT_HD bool find_by_pos(u32 pos, u32& leaf, u32& vstart, u32& blk, u32& i) const {
     u32 g, base;
     if (!w.root_find_pos(s.ng, pos, g, base)) return false;
-    u32 blk = w.root_blk(g);
-    u32 i, before;
-    if (!w.blk_find_pos(dvis(blk), w.root_cnt(g), pos - base, i, before)) return false;
-    leaf = w.ld(dleaf(blk) + i);
+    blk = w.root_blk(g);
+    u32 before;
+    if (!w.blk_find_pos(dvis(blk), dleaf(blk), w.root_cnt(g), pos - base, i, before, leaf)) return false;
     vstart = base + before;
     return true;
   }
@@ -155,35 +191,42 @@ struct Replayer {
   CRDT_HD void commit() {
     if (c_leaf == INVALID || !c_dirty) return;
     w.cache_store(leafptr(c_leaf), c_n);
-    u32 v = w.cache_vis(0, c_n);
-    if (v != c_vis) { dir_add_vis(c_leaf, (i64)v - (i64)c_vis); c_vis = v; }
+    dir_set_cached_vis(c_now);
     c_dirty = false;
   }
-  CRDT_HD void ensure(u32 leaf) {
-    if (leaf == c_leaf) return;
+  CRDT_HD void load_cache(u32 leaf, u32 blk, u32 i) {
     commit();
     c_n = w.cache_load(leafptr(leaf));
     c_leaf = leaf;
+    c_blk = blk;
+    c_i = i;
     c_dirty = false;
-    c_vis = w.cache_vis(0, (u32)L);
+    c_now = c_vis = w.cache_vis(0, (u32)L);
     c_vs_ok = false;
+  }
+  CRDT_HD void ensure(u32 leaf) {
+    if (leaf == c_leaf) return;
+    u32 v = w.ld(sol() + leaf);
+    load_cache(leaf, v >> 6, v & 63u);
   }
   CRDT_HD Span get(u32 leaf, u32 idx) {
     ensure(leaf);
     return w.cget(idx);
   }
+  // set entry idx of the cached leaf (tracks the cached visible count exactly)
   CRDT_HD void set(u32 idx, const Span& e) {
+    c_now = c_now - clen(w.cget(idx)) + clen(e);
     w.cset(idx, e);
     c_dirty = true;
   }
+  CRDT_HD u32 cur_len() const { return s.len + c_now - c_vis; }
 
   // ------------------------------------------------------------------ order -> leaf map
-  // ListCRDT::notify (doc.rs:143-153): all orders of `e` now live in `leaf`.
-  CRDT_HD void notify(const Span& e, u32 leaf) {
-    if (!track) return;
-    u32* m = P.leaf_of + seg.map_base + e.order;
-    if (w.ld(m) == leaf) return;  // run already mapped to this leaf
-    w.fill(m, slen(e), leaf);
+  // ListCRDT::notify (doc.rs:143-153): all orders of `e` now live in `leaf`.  `home` is the
+  // leaf the run already lives in (INVALID for freshly inserted orders): no write if unchanged.
+  CRDT_HD void notify(const Span& e, u32 leaf, u32 home) {
+    if (!track || home == leaf) return;
+    w.fill(P.leaf_of + seg.map_base + e.order, slen(e), leaf);
   }
 
   // ------------------------------------------------------------------ cursor ops
@@ -241,11 +284,11 @@ struct Replayer {
   }
   // root.rs:54-88 + 401-411, leaf.rs:61-84 (stick_end = false)
   CRDT_HD bool cursor_at_content_pos(u32 pos, Cursor& c) {
-    if (!(c_leaf != INVALID && c_vs_ok && pos >= c_vstart && pos < c_vstart + c_vis)) {
+    if (!(c_leaf != INVALID && c_vs_ok && pos >= c_vstart && pos < c_vstart + c_now)) {
       commit();
-      u32 lf, vs;
-      if (!find_by_pos(pos, lf, vs)) return false;
-      ensure(lf);
+      u32 lf, vs, blk, i;
+      if (!find_by_pos(pos, lf, vs, blk, i)) return false;
+      if (lf != c_leaf) load_cache(lf, blk, i);
       c_vstart = vs;
       c_vs_ok = true;
     }
@@ -258,12 +301,15 @@ struct Replayer {
   CRDT_HD bool get_cursor_before(u32 order, Cursor& c) {
     if (order == ROOT_ORDER) return cursor_at_end(c);
     if (!track || order >= s.next_order) return false;
-    u32 lf = w.ld(P.leaf_of + seg.map_base + order);
-    if (lf == INVALID) return false;
-    ensure(lf);
-    i32 idx = w.cfind_order(c_n, order);
-    if (idx < 0) return false;
-    c = Cursor{lf, (u32)idx, order - w.cget((u32)idx).order};
+    i32 idx = c_leaf != INVALID ? w.cfind_order(c_n, order) : -1;  // cached leaf first: no load
+    if (idx < 0) {
+      u32 lf = w.ld(P.leaf_of + seg.map_base + order);
+      if (lf == INVALID || lf == c_leaf) return false;
+      ensure(lf);
+      idx = w.cfind_order(c_n, order);
+      if (idx < 0) return false;
+    }
+    c = Cursor{c_leaf, (u32)idx, order - w.cget((u32)idx).order};
     return true;
   }
   CRDT_HD bool get_cursor_after(u32 order, Cursor& c) {
@@ -281,20 +327,23 @@ struct Replayer {
     u32 stolen = w.cache_vis(idx, c_n);
     w.cache_write_moved(leafptr(nl), idx, c_n, padding);
     if (track)
-      for (u32 j = idx; j < c_n; j++) notify(w.cget(j), nl);
+      for (u32 j = idx; j < c_n; j++) notify(w.cget(j), nl, INVALID);
     w.cache_clear(idx, c_n);
+    c_now -= stolen;
     c_n = idx;
     c_dirty = true;
-    u32 a = c_leaf;
-    dir_insert_after(a, nl, stolen);
-    dir_add_vis(a, -(i64)stolen);
+    dir_insert_after_cached(nl, stolen);
+    // the cached leaf's directory count loses `stolen` (dir_insert_after added it for nl)
+    w.st(dvis(c_blk) + c_i, c_vis - stolen);
+    w.root_add_vis(w.root_find_blk(s.ng, c_blk), 0u - stolen);
+    s.len -= stolen;
     c_vis -= stolen;
     return nl;
   }
-  // mutations.rs:17-179 insert_internal
-  // items are passed as three named values (n <= 3) so they stay in registers
+  // mutations.rs:17-179 insert_internal.  items: up to three named values (stay in registers);
+  // home: leaf the items already live in (INVALID for fresh orders), for notify().
   CRDT_HD static Span pick(const Span& a, const Span& b, const Span& c, u32 k) { return k == 0 ? a : (k == 1 ? b : c); }
-  CRDT_HD bool insert_internal(Span i0, Span i1, Span i2, u32 nitems, Cursor& c) {
+  CRDT_HD bool insert_internal(Span i0, Span i1, Span i2, u32 nitems, Cursor& c, u32 home) {
     if (nitems == 0) return true;
     u32 ib = 0;  // items[ib .. ib+nitems)
     ensure(c.leaf);
@@ -317,7 +366,7 @@ struct Replayer {
       while (it < nitems) {
         Span nx = pick(i0, i1, i2, ib + it);
         if (!can_append(cur, nx)) break;
-        notify(nx, c.leaf);
+        notify(nx, c.leaf, home);
         cur.len += nx.len;
         c.off = slen(cur);
         it++;
@@ -335,7 +384,7 @@ struct Replayer {
         while (true) {
           Span it2 = pick(i0, i1, i2, ib + end);
           if (!can_append(it2, nx2)) break;
-          notify(it2, c.leaf);
+          notify(it2, c.leaf, home);
           nx2.order = it2.order;  // prepend (span.rs:61-64): origin_left is NOT updated
           nx2.len += it2.len;
           any = true;
@@ -370,23 +419,24 @@ struct Replayer {
     }
     for (u32 k = 0; k < nitems; k++) {
       Span x = pick(i0, i1, i2, ib + k);
-      notify(x, c.leaf);
+      notify(x, c.leaf, home);
       set(c.idx + k, x);
     }
     Span last = pick(i0, i1, i2, ib + nitems - 1);
     c.idx += nitems - 1;
     c.off = slen(last);
     if (has_rem) {
-      if (rem_moved) notify(rem, c.leaf);
+      if (rem_moved) notify(rem, c.leaf, INVALID);
       set(c.idx + 1, rem);
     }
     return true;
   }
   // mutations.rs:185-200 (items = i0 then up to two more)
   CRDT_HD bool replace_entry(Cursor& c, Span i0, Span i1, Span i2, u32 n) {
+    u32 home = c.leaf;
     set(c.idx, i0);
     c.off = slen(i0);
-    return insert_internal(i1, i2, i2, n - 1, c);
+    return insert_internal(i1, i2, i2, n - 1, c, home);
   }
   // mutations.rs:227-277.  del_next != nullptr: local delete, stream the deactivated run into
   // the delete log (extend_delete + Rle::append compose to the same list).
@@ -440,22 +490,37 @@ struct Replayer {
   }
 
   // ------------------------------------------------------------------ RLE side tables
-  CRDT_HD u32 agent_next_seq(u32 agent) const {  // doc.rs:20-24
-    AgentRec A = w.ld_agent(P.agents + seg.agent_base + agent);
-    if (A.run_cnt == 0) return 0;
-    ARun l = w.ld_arun(P.arun + seg.arun_base + A.run_base + A.run_cnt - 1);
-    return l.key + l.len;
+  CRDT_HD void use_agent(u32 a) {  // agent cache (author of the current txn)
+    if (a == ag_id) return;
+    ag_id = a;
+    ag = w.ld_agent(agp(a));
+    if (ag.run_cnt) ag_last = w.ld_arun(arunp(ag) + ag.run_cnt - 1);
+  }
+  CRDT_HD u32 agent_next_seq(u32 agent) {  // doc.rs:20-24
+    use_agent(agent);
+    return ag.run_cnt ? ag_last.key + ag_last.len : 0u;
   }
   CRDT_HD bool seq_to_order(u32 agent, u32 seq, u32& order) const {  // doc.rs:26-29
-    AgentRec A = w.ld_agent(P.agents + seg.agent_base + agent);
-    const ARun* base = P.arun + seg.arun_base + A.run_base;
-    i32 k = w.search_arun(base, A.run_cnt, seq);
+    if (agent == ag_id) {
+      if (ag.run_cnt && seq >= ag_last.key && seq - ag_last.key < ag_last.len) {
+        order = ag_last.order + (seq - ag_last.key);
+        return true;
+      }
+      i32 k = w.search_arun(arunp(ag), ag.run_cnt, seq);
+      if (k < 0) return false;
+      ARun r = w.ld_arun(arunp(ag) + k);
+      order = r.order + (seq - r.key);
+      return true;
+    }
+    AgentRec A = w.ld_agent(agp(agent));
+    i32 k = w.search_arun(arunp(A), A.run_cnt, seq);
     if (k < 0) return false;
-    ARun r = w.ld_arun(base + k);
+    ARun r = w.ld_arun(arunp(A) + k);
     order = r.order + (seq - r.key);
     return true;
   }
   CRDT_HD bool order_to_agent(u32 order, u32& agent) const {  // client_with_order.get()
+    if (s.n_cwo && order >= cwo_last.key && order - cwo_last.key < cwo_last.len) { agent = cwo_last.agent; return true; }
     const CwoRun* base = P.cwo + seg.cwo_base;
     i32 k = w.search_cwo(base, s.n_cwo, order);
     if (k < 0) return false;
@@ -465,36 +530,36 @@ struct Replayer {
   // doc.rs:155-165 assign_order_to_client
   CRDT_HD void assign_order_to_client(u32 agent, u32 seq, u32 order, u32 len) {
     CwoRun* cb = P.cwo + seg.cwo_base;
-    bool merged = false;
-    if (s.n_cwo > 0) {
-      CwoRun l = w.ld_cwo(cb + s.n_cwo - 1);
-      if (order == l.key + l.len && agent == l.agent && seq == l.seq + l.len) {
-        w.st(&cb[s.n_cwo - 1].len, l.len + len);
-        merged = true;
-      }
+    if (s.n_cwo > 0 && order == cwo_last.key + cwo_last.len && agent == cwo_last.agent && seq == cwo_last.seq + cwo_last.len) {
+      cwo_last.len += len;
+      w.st(&cb[s.n_cwo - 1].len, cwo_last.len);
+    } else {
+      cwo_last = CwoRun{order, agent, seq, len};
+      w.st_cwo(cb + s.n_cwo, cwo_last);
+      s.n_cwo++;
     }
-    if (!merged) { w.st_cwo(cb + s.n_cwo, CwoRun{order, agent, seq, len}); s.n_cwo++; }
-    AgentRec* ap = P.agents + seg.agent_base + agent;
-    AgentRec A = w.ld_agent(ap);
-    ARun* rb = P.arun + seg.arun_base + A.run_base;
-    merged = false;
-    if (A.run_cnt > 0) {
-      ARun l = w.ld_arun(rb + A.run_cnt - 1);
-      if (seq == l.key + l.len && order == l.order + l.len) {
-        w.st(&rb[A.run_cnt - 1].len, l.len + len);
-        merged = true;
-      }
+    use_agent(agent);
+    ARun* rb = arunp(ag);
+    if (ag.run_cnt > 0 && seq == ag_last.key + ag_last.len && order == ag_last.order + ag_last.len) {
+      ag_last.len += len;
+      w.st(&rb[ag.run_cnt - 1].len, ag_last.len);
+    } else {
+      ag_last = ARun{seq, order, len, 0};
+      w.st_arun(rb + ag.run_cnt, ag_last);
+      ag.run_cnt++;
+      w.st(&agp(agent)->run_cnt, ag.run_cnt);
     }
-    if (!merged) { w.st_arun(rb + A.run_cnt, ARun{seq, order, len, 0}); w.st(&ap->run_cnt, A.run_cnt + 1); }
     if (track) w.fill(P.leaf_of + seg.map_base + order, len, INVALID);
   }
   CRDT_HD void append_delete(u32 key, u32 target, u32 len) {  // Rle<KVPair<DeleteEntry>>::append
     DelRun* b = P.dels + seg.del_base;
-    if (s.n_del > 0) {
-      DelRun l = w.ld_del(b + s.n_del - 1);
-      if (key == l.key + l.len && l.order + l.len == target) { w.st(&b[s.n_del - 1].len, l.len + len); return; }
+    if (s.n_del > 0 && key == del_last.key + del_last.len && del_last.order + del_last.len == target) {
+      del_last.len += len;
+      w.st(&b[s.n_del - 1].len, del_last.len);
+      return;
     }
-    w.st_del(b + s.n_del, DelRun{key, target, len});
+    del_last = DelRun{key, target, len};
+    w.st_del(b + s.n_del, del_last);
     s.n_del++;
   }
   // double_delete.rs:41-107 increment_delete_range (rare path; scalar)
@@ -558,48 +623,61 @@ struct Replayer {
     }
     return true;
   }
-  // doc.rs:350-374 insert_txn (+ advance_branch_by :34-48).  Parents already written to the
-  // pool at [n_par, n_par + np).
-  CRDT_HD i32 insert_txn(bool remote, u32 first, u32 len, u32 np) {
+  CRDT_HD bool par_contains(const u32* par, u32 np, u32 p0, u32 x) const {
+    if (np == 0) return false;
+    if (p0 == x) return true;
+    for (u32 j = 1; j < np; j++) if (w.ld(par + j) == x) return true;
+    return false;
+  }
+  // doc.rs:350-374 insert_txn (+ advance_branch_by :34-48).  Remote parents are already in the
+  // pool at [n_par, n_par + np), the first one also in p0.
+  CRDT_HD i32 insert_txn(bool remote, u32 first, u32 len, u32 np, u32 p0) {
     u32* fr = P.frontier + seg.fr_base;
     u32* par = P.parents + seg.par_base + s.n_par;
     u32 last = first + len - 1;
     if (remote) {
-      for (u32 k = 0; k < s.n_fr; k++) if (w.ld(fr + k) == first) return ST_FRONTIER;
-      u32 m = 0;
-      for (u32 k = 0; k < s.n_fr; k++) {
-        u32 o = w.ld(fr + k);
-        bool in = false;
-        for (u32 j = 0; j < np; j++) if (w.ld(par + j) == o) { in = true; break; }
-        if (!in) { w.st(fr + m, o); m++; }
+      if (s.n_fr == 1) {
+        if (fr0 == first) return ST_FRONTIER;
+        if (par_contains(par, np, p0, fr0)) { fr0 = last; w.st(fr, last); }
+        else { w.st(fr + 1, last); s.n_fr = 2; }
+      } else {
+        for (u32 k = 0; k < s.n_fr; k++) if (w.ld(fr + k) == first) return ST_FRONTIER;
+        u32 m = 0;
+        for (u32 k = 0; k < s.n_fr; k++) {
+          u32 o = w.ld(fr + k);
+          if (!par_contains(par, np, p0, o)) { w.st(fr + m, o); m++; }
+        }
+        if (m + 1 > FRONTIER_CAP) return ST_CAPACITY;
+        w.st(fr + m, last);
+        s.n_fr = m + 1;
+        fr0 = w.ld(fr);
       }
-      if (m + 1 > FRONTIER_CAP) return ST_CAPACITY;
-      w.st(fr + m, last);
-      s.n_fr = m + 1;
     } else {
       np = s.n_fr;
-      for (u32 k = 0; k < np; k++) w.st(par + k, w.ld(fr + k));
+      p0 = fr0;
+      w.st(par, fr0);
+      for (u32 k = 1; k < np; k++) w.st(par + k, w.ld(fr + k));
       w.st(fr, last);
+      fr0 = last;
       s.n_fr = 1;
     }
     u32 shadow = first;
     TxnRec* tb = P.txns + seg.txn_base;
-    while (shadow >= 1) {
-      bool in = false;
-      for (u32 j = 0; j < np; j++) if (w.ld(par + j) == shadow - 1) { in = true; break; }
-      if (!in) break;
-      i32 k = w.search_txn(tb, s.n_txn, shadow - 1);
+    while (shadow >= 1 && par_contains(par, np, p0, shadow - 1)) {
+      u32 x = shadow - 1;
+      if (s.n_txn && x >= txn_last.order && x - txn_last.order < txn_last.len) { shadow = txn_last.shadow; continue; }
+      i32 k = w.search_txn(tb, s.n_txn, x);
       if (k < 0) return ST_UNKNOWN_ID;
       shadow = w.ld(&tb[k].shadow);
     }
-    if (s.n_txn > 0) {
-      TxnRec l = w.ld_txn(tb + s.n_txn - 1);
-      if (np == 1 && w.ld(par) == l.order + l.len - 1 && shadow == l.shadow) {
-        w.st(&tb[s.n_txn - 1].len, l.len + len);
-        return ST_OK;  // parents of a merged txn are not kept
-      }
+    if (s.n_txn > 0 && np == 1 && p0 == txn_last.order + txn_last.len - 1 && shadow == txn_last.shadow) {
+      txn_last.len += len;
+      w.st(&tb[s.n_txn - 1].len, txn_last.len);
+      return ST_OK;  // parents of a merged txn are not kept
     }
-    w.st_txn(tb + s.n_txn, TxnRec{first, len, shadow, s.n_par, np, {0, 0, 0}});
+    txn_last = TxnRec{first, len, shadow, s.n_par, np, {0, 0, 0}};
+    txn_last_p0 = p0;
+    w.st_txn(tb + s.n_txn, txn_last);
     s.n_txn++;
     s.n_par += np;
     return ST_OK;
@@ -627,8 +705,8 @@ struct Replayer {
       if (c == 0) {
         u32 oa;
         if (!order_to_agent(other_entry.order, oa)) return ST_UNKNOWN_ID;
-        if (!have_rank) { my_rank = w.ld_agent(P.agents + seg.agent_base + agent).rank; have_rank = true; }
-        u32 other_rank = w.ld_agent(P.agents + seg.agent_base + oa).rank;
+        if (!have_rank) { my_rank = w.ld_agent(agp(agent)).rank; have_rank = true; }
+        u32 other_rank = w.ld_agent(agp(oa)).rank;
         if (my_rank > other_rank) scanning = false;
         else if (item.orr == other_entry.orr) break;
         else { scanning = true; scan_start = cursor; }
@@ -637,7 +715,7 @@ struct Replayer {
     }
     if (scanning) cursor = scan_start;
     // RangeTree::insert (mutations.rs:202-224)
-    if (!insert_internal(item, item, item, 1, cursor)) return ST_INTERNAL;
+    if (!insert_internal(item, item, item, 1, cursor, INVALID)) return ST_INTERNAL;
     s.n_items += (u32)item.len;
     return ST_OK;
   }
@@ -650,26 +728,25 @@ struct Replayer {
   }
 
   // ------------------------------------------------------------------ txn application
-  // Capacity needed by a txn of n_ops ops / txn_len orders (checked before any mutation, so a
-  // capacity stop is resumable at this txn).
+  // Capacity needed by a txn (checked before any mutation, so a capacity stop is resumable at
+  // this txn).  Every block but the first holds >= 32 slots, so blk_cap = leaf_cap/32 + 2 and
+  // leaf_cap <= 32*(MAX_GROUPS-1) (host-enforced) bound blocks and root groups as well.
+  // On failure s.cap_need records which table (bit) must grow.
   CRDT_HD bool fits(bool remote, u32 agent, u32 n_ops, u32 n_dels, u32 txn_len, u32 n_parents) {
-    // every block but the first holds >= 32 slots, so blk_cap = leaf_cap/32 + 2 and
-    // leaf_cap <= 32*(MAX_GROUPS-1) (host-enforced) bound blocks and root groups as well.
-    // On failure s.cap_need records which table (bit) must grow; the txn is not started.
     u32 need = 0;
     if ((u64)s.n_leaves + 2ull * n_ops > seg.leaf_cap) need |= 1u;
     if (s.n_cwo + 1 > seg.cwo_cap || s.n_txn + 1 > seg.txn_cap) need |= 2u;
     if ((u64)s.n_del + n_dels > seg.del_cap) need |= 4u;
     if ((u64)s.n_par + (remote ? n_parents : s.n_fr) > seg.par_cap) need |= 8u;
     if (track && (u64)s.next_order + txn_len > seg.map_cap) need |= 16u;
-    AgentRec A = w.ld_agent(P.agents + seg.agent_base + agent);
-    if (A.run_cnt + 1 > A.run_cap) need |= 32u;
+    use_agent(agent);
+    if (ag.run_cnt + 1 > ag.run_cap) need |= 32u;
     s.cap_need = need;
     return need == 0;
   }
 
-  // doc.rs:376-469 apply_local_txn.  `r` = LTXN header; ops follow.
-  CRDT_HD i32 apply_local_txn(const Rec& hdr, const Rec* ops) {
+  // doc.rs:376-469 apply_local_txn.  Header at record `pos`; ops follow.
+  CRDT_HD i32 apply_local_txn(const Rec& hdr, u32 pos) {
     u32 nops = hdr.w0 & 0x0FFFFFFFu;
     u32 agent = hdr.w1;
     u32 span = hdr.w3;
@@ -681,13 +758,12 @@ struct Replayer {
     assign_order_to_client(agent, agent_next_seq(agent), first, span);
     s.next_order = first + span;
     for (u32 k = 0; k < nops; k++) {
-      Rec op = w.ld_rec(ops + k);
-      u32 pos = op.w1, del = op.w2, ins = op.w3;
+      Rec op = rec(pos + 1 + k);
+      u32 p = op.w1, del = op.w2, ins = op.w3;
       if (del > 0) {
-        commit();
-        if ((u64)pos + del > s.len) return ST_POS_OOB;
+        if ((u64)p + del > cur_len()) return ST_POS_OOB;
         Cursor c;
-        if (!cursor_at_content_pos(pos, c)) return ST_POS_OOB;
+        if (!cursor_at_content_pos(p, c)) return ST_POS_OOB;
         u32 before = next;
         i32 st = local_deactivate(c, del, next);
         if (st != ST_OK) return st;
@@ -698,11 +774,10 @@ struct Replayer {
         next += ins;
         u32 ol;
         Cursor c;
-        commit();
-        if (pos == 0) { ol = ROOT_ORDER; c = cursor_at_start(); }
+        if (p == 0) { ol = ROOT_ORDER; c = cursor_at_start(); }
         else {
-          if (pos > s.len) return ST_POS_OOB;
-          if (!cursor_at_content_pos(pos - 1, c)) return ST_POS_OOB;
+          if (p > cur_len()) return ST_POS_OOB;
+          if (!cursor_at_content_pos(p - 1, c)) return ST_POS_OOB;
           if (!get_item(c, ol)) return ST_POS_OOB;
           if (!next_item(c)) return ST_POS_OOB;
         }
@@ -714,12 +789,11 @@ struct Replayer {
       }
     }
     if (next != first + span) return ST_BAD_INPUT;
-    commit();
-    return insert_txn(false, first, span, 0);
+    return insert_txn(false, first, span, 0, 0);
   }
 
-  // doc.rs:242-348 apply_remote_txn.  ops then parents follow the RTXN header.
-  CRDT_HD i32 apply_remote_txn(const Rec& hdr, const Rec* ops) {
+  // doc.rs:242-348 apply_remote_txn.  Header at record `pos`; ops then parents follow.
+  CRDT_HD i32 apply_remote_txn(const Rec& hdr, u32 pos) {
     u32 nops = hdr.w0 & 0x07FFFFFFu;
     bool zero_op = (hdr.w0 >> 27) & 1u;
     u32 agent = hdr.w1 & 0xFFFFu;
@@ -736,10 +810,9 @@ struct Replayer {
     assign_order_to_client(agent, seq, first, txn_len);
     s.next_order = first + txn_len;
     for (u32 k = 0; k < nops; k++) {
-      Rec op = w.ld_rec(ops + k);
+      Rec op = rec(pos + 1 + k);
       u32 kind = rec_kind(op);
       u32 len = op.w0 & 0x0FFFFFFFu;
-      commit();
       if (kind == REC_RINS) {
         u32 order = next;
         next += len;
@@ -776,36 +849,36 @@ struct Replayer {
         return ST_BAD_INPUT;
       }
     }
-    commit();
     u32* par = P.parents + seg.par_base + s.n_par;
+    u32 p0 = 0;
     for (u32 k = 0; k < np; k++) {
-      Rec pr = w.ld_rec(ops + nops + k);
+      Rec pr = rec(pos + 1 + nops + k);
       if (rec_kind(pr) != REC_RPARENT) return ST_BAD_INPUT;
       u32 o;
       i32 st = id_to_order(pr.w1 & 0xFFFFu, pr.w2, o);
       if (st != ST_OK) return st;
       w.st(par + k, o);
+      if (k == 0) p0 = o;
     }
-    return insert_txn(true, first, txn_len, np);
+    return insert_txn(true, first, txn_len, np, p0);
   }
 
   // Replay this document's record stream from s.rec_pos.
   CRDT_HD void run() {
-    const Rec* rb = P.recs + seg.rec_base;
     u32 pos = s.rec_pos;
     while (s.status == ST_OK && pos < seg.rec_n) {
-      Rec h = w.ld_rec(rb + pos);
+      Rec h = rec(pos);
       u32 kind = rec_kind(h);
       i32 st;
       u32 consumed;
       if (kind == REC_LTXN) {
         u32 nops = h.w0 & 0x0FFFFFFFu;
         consumed = 1 + nops;
-        st = (pos + consumed <= seg.rec_n) ? apply_local_txn(h, rb + pos + 1) : ST_BAD_INPUT;
+        st = (pos + consumed <= seg.rec_n) ? apply_local_txn(h, pos) : ST_BAD_INPUT;
       } else if (kind == REC_RTXN) {
         u32 nops = h.w0 & 0x07FFFFFFu;
         consumed = 1 + nops + (h.w1 >> 16);
-        st = (pos + consumed <= seg.rec_n) ? apply_remote_txn(h, rb + pos + 1) : ST_BAD_INPUT;
+        st = (pos + consumed <= seg.rec_n) ? apply_remote_txn(h, pos) : ST_BAD_INPUT;
       } else {
         st = ST_BAD_INPUT;
         consumed = 1;

@@ -185,11 +185,23 @@ struct WaveGPU {
     u32 l = lane_id();
     if (l >= a && l < b) { eo = el = er = 0; en = 0; }
   }
+  // entries [idx, n) move to [idx+k, n+k); the vacated slots [idx, idx+k) become empty
   __device__ __forceinline__ void cache_shift_right(u32 idx, u32 n, u32 k) {
     u32 l = lane_id();
     u32 src = l - k;
     u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
     if (l >= idx + k && l < n + k) { eo = o; el = a; er = b; en = (i32)c; }
+    else if (l >= idx && l < idx + k) { eo = el = er = 0; en = 0; }
+  }
+
+  // ---------------------------------------------------------------- record prefetch (64 per load)
+  u32 rx = 0, ry = 0, rz = 0, rw = 0;
+  __device__ __forceinline__ void rec_block_load(const Rec* p, u32 n) {
+    u32 l = lane_id();
+    if (l < n) { uint4 v = *(const uint4*)(p + l); rx = v.x; ry = v.y; rz = v.z; rw = v.w; }
+  }
+  __device__ __forceinline__ Rec rec_get(u32 k) const {
+    return Rec{rdlane(rx, k), rdlane(ry, k), rdlane(rz, k), rdlane(rw, k)};
   }
 
   // ---------------------------------------------------------------- directory root (VGPRs)
@@ -277,14 +289,18 @@ struct WaveGPU {
   }
 
   // ---------------------------------------------------------------- directory blocks (HBM)
-  __device__ __forceinline__ bool blk_find_pos(const u32* dv, u32 cnt, u32 rem, u32& i, u32& before) const {
+  // slot of a block whose cumulative visible count first exceeds rem (+ its leaf id; both block
+  // rows are loaded together so the descent costs one HBM round trip)
+  __device__ __forceinline__ bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
     u32 l = lane_id();
-    u32 x = l < cnt ? *(const u32*)(dv + l) : 0u;
+    u32 x = 0, lf = 0;
+    if (l < cnt) { x = dv[l]; lf = dl[l]; }
     u32 incl = wave_incl_scan(x);
     u32 k = __popcll(ballot(l < cnt && incl <= rem));
     if (k >= cnt) return false;
     i = k;
     before = rdlane(incl, k) - rdlane(x, k);
+    leaf = rdlane(lf, k);
     return true;
   }
   __device__ __forceinline__ void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
