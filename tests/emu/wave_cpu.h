@@ -67,10 +67,19 @@ struct WaveCPU {
     for (u32 i = 0; i < (u32)L; i++) n += c[i].len != 0;
     return n;
   }
-  void cache_store(Span* p, u32) const { for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
+  void cache_store(Span* p) const { for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
   Span cget(u32 i) const { return c[i & 63]; }
+  u32 cget_order(u32 i) const { return c[i & 63].order; }
+  i32 cget_len(u32 i) const { return c[i & 63].len; }
   void cset(u32 i, const Span& s) { c[i & 63] = s; }
-  u32 cache_vis(u32 a, u32 b) const { u32 t = 0; for (u32 i = a; i < b && i < 64; i++) t += clen(c[i]); return t; }
+  u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
+  u64 lanes_in(u32 a, u32 b) const { u64 m = 0; for (u32 i = a; i < b && i < 64; i++) m |= 1ull << i; return m; }
+  static u32 first_lane(u64 m) { return (u32)__builtin_ctzll(m); }
+  i32 peek_find_order(const Span* p, u32 order, u32& start) const {
+    for (u32 i = 0; i < (u32)L; i++)
+      if (p[i].len != 0 && order >= p[i].order && order - p[i].order < slen(p[i])) { start = p[i].order; return (i32)i; }
+    return -1;
+  }
   bool cfind_content(u32 n, u32 rem, u32& idx, u32& off) const {
     for (u32 i = 0; i < n; i++) {
       u32 e = clen(c[i]);

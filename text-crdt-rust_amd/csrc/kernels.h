@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void k_init(Pools P, u32 n) {
   WaveGPU<L> w;
   Replayer<WaveGPU<L>, L> r(w, P, d);
   r.init_empty();
-  for (u32 a = lane_id(); a < r.s.n_agents; a += 64) P.agents[r.seg.agent_base + a].run_cnt = 0;
+  for (u32 a = lane_id(); a < r.s.n_agents; a += 64) r.agents[a].run_cnt = 0;
   r.finish();
 }
 
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void k_replay(Pools P, u32 n) {
   WaveGPU<L> w;
   Replayer<WaveGPU<L>, L> r(w, P, d);
   if (r.s.status == ST_NEED_CAPACITY) r.s.status = ST_OK;  // resume after growth
-  if (r.s.status != ST_OK || r.s.rec_pos >= r.seg.rec_n) {
+  if (r.s.status != ST_OK || r.s.rec_pos >= r.rec_n) {
     w.st((u32*)&P.st[d].status, (u32)r.s.status);
     return;
   }

@@ -85,6 +85,7 @@ struct WaveGPU {
 
   // lane-parallel fill of n u32
   __device__ __forceinline__ void fill(u32* p, u32 n, u32 v) const {
+    if (n == 1) { *p = v; return; }  // the common single-item case: one coalesced store
     for (u32 k = lane_id(); k < n; k += 64) p[k] = v;
   }
   __device__ __forceinline__ void zero_leaf(Span* p, u32 n) const {
@@ -137,20 +138,41 @@ struct WaveGPU {
     } else { eo = el = er = 0; en = 0; }
     return __popcll(ballot(l < (u32)L && en != 0));
   }
-  __device__ __forceinline__ void cache_store(Span* p, u32 /*n*/) const {
+  __device__ __forceinline__ void cache_store(Span* p) const {
     u32 l = lane_id();
     if (l < (u32)L) *(uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
   }
   __device__ __forceinline__ Span cget(u32 i) const {
     return Span{rdlane(eo, i), rdlane(el, i), rdlane(er, i), (i32)rdlane((u32)en, i)};
   }
-  __device__ __forceinline__ void cset(u32 i, const Span& s) {
-    if (lane_id() == i) { eo = s.order; el = s.ol; er = s.orr; en = s.len; }
+  __device__ __forceinline__ u32 cget_order(u32 i) const { return rdlane(eo, i); }
+  __device__ __forceinline__ i32 cget_len(u32 i) const { return (i32)rdlane((u32)en, i); }
+  __device__ __forceinline__ void cset(u32 i, const Span& s) {  // branch-free: 4 v_cndmask
+    bool me = lane_id() == i;
+    eo = me ? s.order : eo;
+    el = me ? s.ol : el;
+    er = me ? s.orr : er;
+    en = me ? s.len : en;
+  }
+  // lanes [a, b) as a mask, and the lowest lane of a mask (wave-uniform)
+  __device__ __forceinline__ u64 lanes_in(u32 a, u32 b) const { u32 l = lane_id(); return ballot(l >= a && l < b); }
+  __device__ __forceinline__ static u32 first_lane(u64 m) { return (u32)__builtin_ctzll(m); }
+  // leaf.rs:41-57 find on a leaf that is NOT the cached one (peek: no cache change)
+  __device__ __forceinline__ i32 peek_find_order(const Span* p, u32 order, u32& start) const {
+    u32 l = lane_id();
+    u32 o = 0;
+    i32 n = 0;
+    if (l < (u32)L) { uint4 v = *(const uint4*)(p + l); o = v.x; n = (i32)v.w; }
+    u32 sl = (u32)(n < 0 ? -n : n);
+    u64 m = ballot(l < (u32)L && n != 0 && order >= o && order - o < sl);
+    if (!m) return -1;
+    u32 k = (u32)__builtin_ctzll(m);
+    start = rdlane(o, k);
+    return (i32)k;
   }
   __device__ __forceinline__ u32 clen_l() const { return en > 0 ? (u32)en : 0u; }
-  __device__ __forceinline__ u32 cache_vis(u32 a, u32 b) const {
-    u32 l = lane_id();
-    return wave_sum((l >= a && l < b) ? clen_l() : 0u);
+  __device__ __forceinline__ u32 cache_vis_from(u32 a) const {  // visible items in lanes >= a
+    return wave_sum(lane_id() >= a ? clen_l() : 0u);
   }
   // leaf.rs:61-84 find_offset (stick_end = false) over clen
   __device__ __forceinline__ bool cfind_content(u32 n, u32 rem, u32& idx, u32& off) const {
@@ -183,15 +205,23 @@ struct WaveGPU {
   }
   __device__ __forceinline__ void cache_clear(u32 a, u32 b) {
     u32 l = lane_id();
-    if (l >= a && l < b) { eo = el = er = 0; en = 0; }
+    bool z = l >= a && l < b;
+    eo = z ? 0u : eo;
+    el = z ? 0u : el;
+    er = z ? 0u : er;
+    en = z ? 0 : en;
   }
   // entries [idx, n) move to [idx+k, n+k); the vacated slots [idx, idx+k) become empty
   __device__ __forceinline__ void cache_shift_right(u32 idx, u32 n, u32 k) {
     u32 l = lane_id();
     u32 src = l - k;
     u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
-    if (l >= idx + k && l < n + k) { eo = o; el = a; er = b; en = (i32)c; }
-    else if (l >= idx && l < idx + k) { eo = el = er = 0; en = 0; }
+    bool mv = l >= idx + k && l < n + k;
+    bool z = l >= idx && l < idx + k;
+    eo = mv ? o : (z ? 0u : eo);
+    el = mv ? a : (z ? 0u : el);
+    er = mv ? b : (z ? 0u : er);
+    en = mv ? (i32)c : (z ? 0 : en);
   }
 
   // ---------------------------------------------------------------- record prefetch (64 per load)
