@@ -123,8 +123,7 @@ struct EmuDoc {
     bool first = true;
     while (true) {
       Pools p = pools();
-      WaveCPU<LL> w;
-      Replayer<WaveCPU<LL>, LL> r(w, p, 0);
+      Replayer<WaveCPU<LL>, LL> r(p, 0);
       if (first) { r.init_empty(); r.s.n_agents = (u32)agents.names.size(); first = false; }
       else { r.s.status = ST_OK; r.begin(); }
       r.run();

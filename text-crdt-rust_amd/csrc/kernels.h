@@ -22,12 +22,21 @@ struct PubOut {
 
 #define WAVES_PER_BLOCK 4
 
+// LDS slice (directory root level) of the calling wave: blk/cnt/vis x MAX_GROUPS u32
+#define ROOT_LDS __shared__ u32 s_root[WAVES_PER_BLOCK][3 * MAX_GROUPS]
+template <int L>
+__device__ __forceinline__ WaveGPU<L> wave_with_root(u32 (*s_root)[3 * MAX_GROUPS]) {
+  WaveGPU<L> w;
+  w.rt = s_root[uni(threadIdx.x >> 6)];
+  return w;
+}
+
 template <int L>
 __global__ __launch_bounds__(256) void k_init(Pools P, u32 n) {
   u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
   if (d >= n) return;
-  WaveGPU<L> w;
-  Replayer<WaveGPU<L>, L> r(w, P, d);
+  ROOT_LDS;
+  Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(s_root));
   r.init_empty();
   for (u32 a = lane_id(); a < r.s.n_agents; a += 64) r.agents[a].run_cnt = 0;
   r.finish();
@@ -37,8 +46,9 @@ template <int L>
 __global__ __launch_bounds__(256) void k_replay(Pools P, u32 n) {
   u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
   if (d >= n) return;
-  WaveGPU<L> w;
-  Replayer<WaveGPU<L>, L> r(w, P, d);
+  ROOT_LDS;
+  Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(s_root));
+  WaveGPU<L>& w = r.w;
   if (r.s.status == ST_NEED_CAPACITY) r.s.status = ST_OK;  // resume after growth
   if (r.s.status != ST_OK || r.s.rec_pos >= r.rec_n) {
     w.st((u32*)&P.st[d].status, (u32)r.s.status);
@@ -116,7 +126,8 @@ template <int L>
 __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
   if (d >= n) return;
-  WaveGPU<L> w;
+  ROOT_LDS;
+  WaveGPU<L> w = wave_with_root<L>(s_root);
   DocState s = w.ldT(P.st + d);
   DocSeg seg = P.seg[d];
   u32 l = lane_id();

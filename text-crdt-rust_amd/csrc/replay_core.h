@@ -38,7 +38,7 @@ struct Cursor {
 
 template <class W, int L>
 struct Replayer {
-  W& w;
+  W w;  // owned by value: its lane registers must stay SSA values, never a scratch object
   // ---- this document's tables (Pools + DocSeg bases, resolved once)
   Span* lv;
   u32* dl;
@@ -81,7 +81,7 @@ struct Replayer {
   // ---- record prefetch
   u32 rb_base = 0x80000000u;  // pos - rb_base >= 64 for every valid pos
 
-  CRDT_HD Replayer(W& w_, const Pools& P, u32 d) : w(w_) {
+  CRDT_HD Replayer(const Pools& P, u32 d, const W& w0 = W()) : w(w0) {
     DocSeg g = w.ld_seg(P.seg + d);
     lv = P.leaves + g.leaf_base * (u64)L;
     dl = P.dir_leaf + g.blk_base * (u64)GROUP;

@@ -29,21 +29,16 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
 }
 __device__ __forceinline__ u32 wave_sum(u32 v) { return rdlane(wave_incl_scan(v), 63); }
 
-struct Slots4 {  // 4 VGPRs indexed by a wave-uniform register number
-  u32 r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-  __device__ __forceinline__ u32 get(u32 r) const { return r == 0 ? r0 : r == 1 ? r1 : r == 2 ? r2 : r3; }
-  __device__ __forceinline__ void put(u32 r, u32 v) {
-    if (r == 0) r0 = v; else if (r == 1) r1 = v; else if (r == 2) r2 = v; else r3 = v;
-  }
-};
-
 template <int L>
 struct WaveGPU {
   // ---------------------------------------------------------------- leaf cache
   u32 eo = 0, el = 0, er = 0;
   i32 en = 0;
-  // ---------------------------------------------------------------- root level
-  Slots4 gb, gc, gv;
+  // ---------------------------------------------------------------- root level (LDS)
+  // This wave's slice of the kernel's LDS: blk[MAX_GROUPS], cnt[MAX_GROUPS], vis[MAX_GROUPS]
+  // (structure of arrays: lane-parallel sweeps are bank-conflict free).  Kept out of VGPRs so
+  // that no register is ever indexed by a run-time group number.
+  u32* rt = nullptr;
 
   // ---- scalar memory helpers (every lane touches the same address: uniform results, and a
   //      store is then visible to every lane's later loads by per-thread program order)
@@ -235,18 +230,25 @@ struct WaveGPU {
   }
 
   // ---------------------------------------------------------------- directory root (VGPRs)
+  __device__ __forceinline__ u32* rblk() const { return rt; }
+  __device__ __forceinline__ u32* rcnt() const { return rt + MAX_GROUPS; }
+  __device__ __forceinline__ u32* rvis() const { return rt + 2 * MAX_GROUPS; }
   __device__ __forceinline__ void root_init(u32 blk, u32 cnt, u32 vis) {
-    gb = Slots4(); gc = Slots4(); gv = Slots4();
-    if (lane_id() == 0) { gb.r0 = blk; gc.r0 = cnt; gv.r0 = vis; }
+    rblk()[0] = blk;  // every lane stores the same value: no branch
+    rcnt()[0] = cnt;
+    rvis()[0] = vis;
   }
   __device__ __forceinline__ void root_load(const GroupRec* g, u32 ng) {
     u32 l = lane_id();
 #pragma unroll
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       u32 i = r * 64 + l;
-      u32 b = 0, c = 0, v = 0;
-      if (i < ng) { uint4 x = *(const uint4*)(g + i); b = x.x; c = x.y; v = x.z; }
-      gb.put(r, b); gc.put(r, c); gv.put(r, v);
+      if (i < ng) {
+        uint4 x = *(const uint4*)(g + i);
+        rblk()[i] = x.x;
+        rcnt()[i] = x.y;
+        rvis()[i] = x.z;
+      }
     }
   }
   __device__ __forceinline__ void root_store(GroupRec* g, u32 ng) const {
@@ -254,46 +256,52 @@ struct WaveGPU {
 #pragma unroll
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       u32 i = r * 64 + l;
-      if (i < ng) *(uint4*)(g + i) = make_uint4(gb.get(r), gc.get(r), gv.get(r), 0);
+      if (i < ng) *(uint4*)(g + i) = make_uint4(rblk()[i], rcnt()[i], rvis()[i], 0);
     }
   }
-  __device__ __forceinline__ u32 root_blk(u32 g) const { return rdlane(gb.get(g >> 6), g & 63); }
-  __device__ __forceinline__ u32 root_cnt(u32 g) const { return rdlane(gc.get(g >> 6), g & 63); }
-  __device__ __forceinline__ u32 root_vis(u32 g) const { return rdlane(gv.get(g >> 6), g & 63); }
+  __device__ __forceinline__ u32 root_blk(u32 g) const { return uni(rblk()[g]); }
+  __device__ __forceinline__ u32 root_cnt(u32 g) const { return uni(rcnt()[g]); }
+  __device__ __forceinline__ u32 root_vis(u32 g) const { return uni(rvis()[g]); }
   __device__ __forceinline__ u32 root_find_blk(u32 ng, u32 blk) const {
     u32 l = lane_id();
 #pragma unroll
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       if (r * 64 >= ng) break;
-      u64 m = ballot(r * 64 + l < ng && gb.get(r) == blk);
+      u32 i = r * 64 + l;
+      u64 m = ballot(i < ng && rblk()[i] == blk);
       if (m) return r * 64 + __builtin_ctzll(m);
     }
     return INVALID;
   }
   __device__ __forceinline__ void root_add_vis(u32 g, u32 delta) {
-    u32 r = g >> 6;
-    if (lane_id() == (g & 63)) gv.put(r, gv.get(r) + delta);
+    u32 v = uni(rvis()[g]) + delta;
+    rvis()[g] = v;
   }
   __device__ __forceinline__ void root_set(u32 g, u32 blk, u32 cnt, u32 vis) {
-    u32 r = g >> 6;
-    if (lane_id() == (g & 63)) { gb.put(r, blk); gc.put(r, cnt); gv.put(r, vis); }
+    rblk()[g] = blk;
+    rcnt()[g] = cnt;
+    rvis()[g] = vis;
   }
-  // insert a group at index g, shifting [g, ng) up by one
+  // insert a group at index g, shifting [g, ng) up by one (read everything, then write)
   __device__ __forceinline__ void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
     u32 l = lane_id();
-    Slots4 nb = gb, nc = gc, nv = gv;
+    u32 b[MAX_GROUP_REGS], c[MAX_GROUP_REGS], v[MAX_GROUP_REGS];
 #pragma unroll
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
-      if (r * 64 > ng) break;
-      u32 pb = r ? rdlane(gb.get(r - 1), 63) : 0u;
-      u32 pc = r ? rdlane(gc.get(r - 1), 63) : 0u;
-      u32 pv = r ? rdlane(gv.get(r - 1), 63) : 0u;
-      u32 sb = shfl(gb.get(r), l - 1), sc = shfl(gc.get(r), l - 1), sv = shfl(gv.get(r), l - 1);
-      if (l == 0) { sb = pb; sc = pc; sv = pv; }
       u32 i = r * 64 + l;
-      if (i > g && i <= ng) { nb.put(r, sb); nc.put(r, sc); nv.put(r, sv); }
+      u32 j = i - 1;
+      bool mv = i > g && i <= ng;
+      b[r] = mv ? rblk()[j] : 0u;
+      c[r] = mv ? rcnt()[j] : 0u;
+      v[r] = mv ? rvis()[j] : 0u;
     }
-    gb = nb; gc = nc; gv = nv;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
+      u32 i = r * 64 + l;
+      if (i > g && i <= ng) { rblk()[i] = b[r]; rcnt()[i] = c[r]; rvis()[i] = v[r]; }
+    }
+    __builtin_amdgcn_wave_barrier();
     root_set(g, blk, cnt, vis);
   }
   // first group whose cumulative visible count exceeds pos
@@ -303,8 +311,9 @@ struct WaveGPU {
 #pragma unroll
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       if (r * 64 >= ng) break;
-      bool valid = r * 64 + l < ng;
-      u32 x = valid ? gv.get(r) : 0u;
+      u32 i = r * 64 + l;
+      bool valid = i < ng;
+      u32 x = valid ? rvis()[i] : 0u;
       u32 incl = wave_incl_scan(x) + carry;
       u32 nvalid = ng - r * 64 < 64 ? ng - r * 64 : 64;
       u32 k = __popcll(ballot(valid && incl <= pos));
