@@ -124,8 +124,8 @@ struct EmuDoc {
     while (true) {
       Pools p = pools();
       Replayer<WaveCPU<LL>, LL> r(p, 0);
-      if (first) { r.init_empty(); r.s.n_agents = (u32)agents.names.size(); first = false; }
-      else { r.s.status = ST_OK; r.begin(); }
+      if (first) { r.init_empty(); r.p(S_N_AGENTS, (u32)agents.names.size()); first = false; }
+      else { r.p(S_STATUS, (u32)ST_OK); r.begin(); }
       r.run();
       r.finish();
       if (st.status != ST_NEED_CAPACITY) break;

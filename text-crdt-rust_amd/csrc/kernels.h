@@ -38,7 +38,8 @@ __global__ __launch_bounds__(256) void k_init(Pools P, u32 n) {
   ROOT_LDS;
   Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(s_root));
   r.init_empty();
-  for (u32 a = lane_id(); a < r.s.n_agents; a += 64) r.agents[a].run_cnt = 0;
+  AgentRec* ag = r.agents();
+  for (u32 a = lane_id(); a < r.g(S_N_AGENTS); a += 64) ag[a].run_cnt = 0;
   r.finish();
 }
 
@@ -49,9 +50,9 @@ __global__ __launch_bounds__(256) void k_replay(Pools P, u32 n) {
   ROOT_LDS;
   Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(s_root));
   WaveGPU<L>& w = r.w;
-  if (r.s.status == ST_NEED_CAPACITY) r.s.status = ST_OK;  // resume after growth
-  if (r.s.status != ST_OK || r.s.rec_pos >= r.rec_n) {
-    w.st((u32*)&P.st[d].status, (u32)r.s.status);
+  if (r.status() == ST_NEED_CAPACITY) r.p(S_STATUS, (u32)ST_OK);  // resume after growth
+  if (r.status() != ST_OK || r.g(S_REC_POS) >= r.rec_n()) {
+    w.st((u32*)&P.st[d].status, (u32)r.status());
     return;
   }
   r.begin();

@@ -8,23 +8,27 @@
 //     -- which leaks into results through YjsSpan::prepend (span.rs:61-64 keeps origin_left) and
 //     the integrate tie-break (doc.rs:207) -- is bit-identical to the reference's;
 //   * a two-level wave directory instead of internal nodes: 64-slot blocks (leaf id + visible
-//     count) in HBM and a root level of up to 256 groups held in VGPRs (lane = group), so every
-//     descent is two wave-wide scans and every leaf insertion one 64-lane shift;
+//     count) in HBM and a root level of up to 256 groups in LDS, so every descent is two
+//     wave-wide scans and every leaf insertion one 64-lane shift;
 //   * a write-back leaf cache in VGPRs (lane i = entry i) that also remembers its directory slot
 //     and visible count, so runs of edits in one leaf touch neither HBM loads nor the directory;
 //     lookups that only need a position in another leaf (integrate's origin compare, the item
 //     after the end of a leaf) peek at that leaf without evicting the cached one;
 //   * an order->leaf table (u32 per order) replacing the SplitList, written only when a run
 //     changes leaf (the reference's notify() semantics);
-//   * register-resident tails of every RLE table (client_with_order, the author's item_orders,
-//     deletes, txns, frontier) and a 64-record prefetch of the op stream, so the common op issues
+//   * tails of every RLE table (client_with_order, the author's item_orders, deletes, txns,
+//     frontier) kept on chip and a 64-record prefetch of the op stream, so the common op issues
 //     no dependent HBM load at all (stores are fire-and-forget).
 //
-// Code shape (what makes this fast on CDNA4): one op interpreter loop per document in which
-// every heavy routine -- integrate's scan, mutate_entry, insert_internal, split_at -- has exactly
-// ONE inlined instance, so the hot loop stays small in the instruction cache and short in
-// register live ranges.  Control flow is wave-uniform; every lane-parallel step goes through the
-// backend W:
+// Code shape (what makes this fast on CDNA4):
+//   * one op interpreter loop per document in which every heavy routine -- integrate's scan,
+//     mutate_entry, insert_internal, split_at -- has exactly ONE inlined instance;
+//   * every piece of per-document state that lives across ops (table pointers, capacities,
+//     DocState, cache bookkeeping, RLE tails) sits in two "context" VGPRs, one field per lane,
+//     read with v_readlane and written with v_writelane at compile-time lane numbers.  Only
+//     op-transient values are SGPRs, so control-flow merges in the interpreter do not shuffle
+//     ~90 scalar registers around (which is what the compiler does with SSA state this size).
+// Control flow is wave-uniform; every lane-parallel step goes through the backend W:
 //   W = WaveGPU (wave_gpu.h, the product) or WaveCPU (tests/emu, a test-only emulation used to
 //   debug this file against the oracle without a GPU).
 #pragma once
@@ -36,223 +40,267 @@ struct Cursor {
   u32 leaf, idx, off;
 };
 
+// Context slots (lane numbers of the two context VGPRs; < 64: first register).
+enum : u32 {
+  // table pointers, 2 slots each
+  P_LV = 0, P_DL = 2, P_DV = 4, P_SOL = 6, P_LOF = 8, P_CWO = 10, P_ARUN = 12, P_DELS = 14,
+  P_DD = 16, P_TXNS = 18, P_PAR = 20, P_FR = 22, P_AGENTS = 24, P_GROUPS = 26, P_RECS = 28, P_STP = 30,
+  // capacities
+  K_LEAF = 32, K_MAP, K_CWO, K_TXN, K_DEL, K_DD, K_PAR, K_RECN,
+  // DocState, field for field (struct order, 20 dwords)
+  S_BASE = 40,
+  S_STATUS = 40, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
+  S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES,
+  // leaf cache bookkeeping
+  C_LEAF = 64, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
+  // RLE tails
+  T_CWO_KEY, T_CWO_AGENT, T_CWO_SEQ, T_CWO_LEN,
+  T_DEL_KEY, T_DEL_ORDER, T_DEL_LEN,
+  T_TX_ORDER, T_TX_LEN, T_TX_SHADOW,
+  T_FR0,
+  T_AG_ID, T_AG_BASE, T_AG_CNT, T_AG_CAP,
+  T_AGL_KEY, T_AGL_ORDER, T_AGL_LEN,
+  T_RB_BASE,
+  N_SLOTS
+};
+static_assert(S_N_ENTRIES - S_BASE + 4 == sizeof(DocState) / 4, "DocState slot mirror");
+static_assert(N_SLOTS <= 128, "two context registers");
+
 template <class W, int L>
 struct Replayer {
-  W w;  // owned by value: its lane registers must stay SSA values, never a scratch object
-  // ---- this document's tables (Pools + DocSeg bases, resolved once)
-  Span* lv;
-  u32* dl;
-  u32* dv;
-  u32* sol;
-  u32* lof;
-  CwoRun* cwo;
-  ARun* arun;
-  DelRun* dels;
-  DDRun* dd;
-  TxnRec* txns;
-  u32* par;
-  u32* fr;
-  AgentRec* agents;
-  GroupRec* groups;
-  const Rec* recs;
-  DocState* stp;
-  u32 cap_leaf, cap_map, cap_cwo, cap_txn, cap_del, cap_dd, cap_par, rec_n;
-  DocState s;
+  W w;  // owned by value: its lane registers stay SSA values, never a scratch object
 
-  // ---- leaf cache bookkeeping (the entries themselves live in W)
-  u32 c_leaf = INVALID;
-  u32 c_n = 0;
-  u32 c_vis = 0;      // visible count of c_leaf as recorded in the directory
-  u32 c_now = 0;      // visible count of the cached entries right now
-  u32 c_blk = 0, c_i = 0;  // directory slot of c_leaf
-  u32 c_vstart = 0;   // visible items before c_leaf (valid if c_vs_ok)
-  bool c_dirty = false;
-  bool c_vs_ok = false;
-
-  // ---- register-resident RLE tails (written through to HBM on every change)
-  CwoRun cwo_last{0, 0, 0, 0};
-  DelRun del_last{0, 0, 0};
-  u32 tx_order = 0, tx_len = 0, tx_shadow = 0;  // last txns entry
-  u32 fr0 = ROOT_ORDER;
-  u32 ag_id = INVALID;  // agent cache (the txn author): its AgentRec and last item_orders run
-  u32 ag_base = 0, ag_cnt = 0, ag_cap = 0;
-  ARun ag_last{0, 0, 0, 0};
-
-  // ---- record prefetch
-  u32 rb_base = 0x80000000u;  // pos - rb_base >= 64 for every valid pos
+  // ------------------------------------------------------------------ context access
+  CRDT_HD u32 g(u32 f) const { return w.xg(f); }
+  CRDT_HD void p(u32 f, u32 v) { w.xs(f, v); }
+  CRDT_HD void inc(u32 f, u32 d = 1) { w.xs(f, w.xg(f) + d); }
+  template <class T> CRDT_HD T* ptr(u32 f) const { return (T*)(((u64)w.xg(f + 1) << 32) | w.xg(f)); }
+  CRDT_HD void pset(u32 f, const void* q) {
+    u64 v = (u64)q;
+    w.xs(f, (u32)v);
+    w.xs(f + 1, (u32)(v >> 32));
+  }
+  CRDT_HD Span* lv() const { return ptr<Span>(P_LV); }
+  CRDT_HD u32* dl() const { return ptr<u32>(P_DL); }
+  CRDT_HD u32* dv() const { return ptr<u32>(P_DV); }
+  CRDT_HD u32* sol() const { return ptr<u32>(P_SOL); }
+  CRDT_HD u32* lof() const { return ptr<u32>(P_LOF); }
+  CRDT_HD CwoRun* cwo() const { return ptr<CwoRun>(P_CWO); }
+  CRDT_HD ARun* arun() const { return ptr<ARun>(P_ARUN); }
+  CRDT_HD DelRun* dels() const { return ptr<DelRun>(P_DELS); }
+  CRDT_HD DDRun* dd() const { return ptr<DDRun>(P_DD); }
+  CRDT_HD TxnRec* txns() const { return ptr<TxnRec>(P_TXNS); }
+  CRDT_HD u32* par() const { return ptr<u32>(P_PAR); }
+  CRDT_HD u32* fr() const { return ptr<u32>(P_FR); }
+  CRDT_HD AgentRec* agents() const { return ptr<AgentRec>(P_AGENTS); }
+  CRDT_HD GroupRec* groups() const { return ptr<GroupRec>(P_GROUPS); }
+  CRDT_HD const Rec* recs() const { return ptr<const Rec>(P_RECS); }
+  CRDT_HD DocState* stp() const { return ptr<DocState>(P_STP); }
+  CRDT_HD i32 status() const { return (i32)g(S_STATUS); }
+  CRDT_HD u32 rec_n() const { return g(K_RECN); }
 
   CRDT_HD Replayer(const Pools& P, u32 d, const W& w0 = W()) : w(w0) {
-    DocSeg g = w.ld_seg(P.seg + d);
-    lv = P.leaves + g.leaf_base * (u64)L;
-    dl = P.dir_leaf + g.blk_base * (u64)GROUP;
-    dv = P.dir_vis + g.blk_base * (u64)GROUP;
-    sol = P.slot_of_leaf + g.leaf_base;
-    lof = P.leaf_of + g.map_base;
-    cwo = P.cwo + g.cwo_base;
-    arun = P.arun + g.arun_base;
-    dels = P.dels + g.del_base;
-    dd = P.dd + g.dd_base;
-    txns = P.txns + g.txn_base;
-    par = P.parents + g.par_base;
-    fr = P.frontier + g.fr_base;
-    agents = P.agents + g.agent_base;
-    groups = P.groups + g.grp_base;
-    recs = P.recs + g.rec_base;
-    stp = P.st + d;
-    cap_leaf = g.leaf_cap;
-    cap_map = g.map_cap;
-    cap_cwo = g.cwo_cap;
-    cap_txn = g.txn_cap;
-    cap_del = g.del_cap;
-    cap_dd = g.dd_cap;
-    cap_par = g.par_cap;
-    rec_n = g.rec_n;
-    s = w.ld_state(stp);
+    DocSeg sg = w.ld_seg(P.seg + d);
+    pset(P_LV, P.leaves + sg.leaf_base * (u64)L);
+    pset(P_DL, P.dir_leaf + sg.blk_base * (u64)GROUP);
+    pset(P_DV, P.dir_vis + sg.blk_base * (u64)GROUP);
+    pset(P_SOL, P.slot_of_leaf + sg.leaf_base);
+    pset(P_LOF, P.leaf_of + sg.map_base);
+    pset(P_CWO, P.cwo + sg.cwo_base);
+    pset(P_ARUN, P.arun + sg.arun_base);
+    pset(P_DELS, P.dels + sg.del_base);
+    pset(P_DD, P.dd + sg.dd_base);
+    pset(P_TXNS, P.txns + sg.txn_base);
+    pset(P_PAR, P.parents + sg.par_base);
+    pset(P_FR, P.frontier + sg.fr_base);
+    pset(P_AGENTS, P.agents + sg.agent_base);
+    pset(P_GROUPS, P.groups + sg.grp_base);
+    pset(P_RECS, P.recs + sg.rec_base);
+    pset(P_STP, P.st + d);
+    p(K_LEAF, sg.leaf_cap);
+    p(K_MAP, sg.map_cap);
+    p(K_CWO, sg.cwo_cap);
+    p(K_TXN, sg.txn_cap);
+    p(K_DEL, sg.del_cap);
+    p(K_DD, sg.dd_cap);
+    p(K_PAR, sg.par_cap);
+    p(K_RECN, sg.rec_n);
+    w.x_load_state(P.st + d, S_BASE);
+    p(C_LEAF, INVALID);
+    p(C_N, 0);
+    p(C_VIS, 0);
+    p(C_NOW, 0);
+    p(C_BLK, 0);
+    p(C_I, 0);
+    p(C_VSTART, 0);
+    p(C_DIRTY, 0);
+    p(C_VS_OK, 0);
+    p(T_CWO_KEY, 0); p(T_CWO_AGENT, 0); p(T_CWO_SEQ, 0); p(T_CWO_LEN, 0);
+    p(T_DEL_KEY, 0); p(T_DEL_ORDER, 0); p(T_DEL_LEN, 0);
+    p(T_TX_ORDER, 0); p(T_TX_LEN, 0); p(T_TX_SHADOW, 0);
+    p(T_FR0, ROOT_ORDER);
+    p(T_AG_ID, INVALID); p(T_AG_BASE, 0); p(T_AG_CNT, 0); p(T_AG_CAP, 0);
+    p(T_AGL_KEY, 0); p(T_AGL_ORDER, 0); p(T_AGL_LEN, 0);
+    p(T_RB_BASE, 0x80000000u);  // pos - rb_base >= 64 for every valid pos
   }
 
-  CRDT_HD Span* leafp(u32 leaf) const { return lv + (u64)leaf * L; }
-  CRDT_HD u32* dleaf(u32 blk) const { return dl + (u64)blk * GROUP; }
-  CRDT_HD u32* dvis(u32 blk) const { return dv + (u64)blk * GROUP; }
+  CRDT_HD Span* leafp(u32 leaf) const { return lv() + (u64)leaf * L; }
+  CRDT_HD u32* dleaf(u32 blk) const { return dl() + (u64)blk * GROUP; }
+  CRDT_HD u32* dvis(u32 blk) const { return dv() + (u64)blk * GROUP; }
 
   // ------------------------------------------------------------------ init / begin / finish
   // New empty document: ListCRDT::new (doc.rs:51-64): one empty root leaf, frontier [ROOT].
   CRDT_HD void init_empty() {
-    s.status = ST_OK;
-    s.rec_pos = 0;
-    s.n_leaves = 1;
-    s.n_blocks = 1;
-    s.ng = 1;
-    s.next_order = 0;
-    s.len = 0;
-    s.n_cwo = s.n_del = s.n_dd = s.n_txn = s.n_par = 0;
-    s.n_fr = 1;
-    s.n_items = 0;
-    s.cap_need = 0;
-    s.n_entries = 0;
+    p(S_STATUS, (u32)ST_OK);
+    p(S_REC_POS, 0);
+    p(S_N_LEAVES, 1);
+    p(S_N_BLOCKS, 1);
+    p(S_NG, 1);
+    p(S_NEXT_ORDER, 0);
+    p(S_LEN, 0);
+    p(S_N_CWO, 0); p(S_N_DEL, 0); p(S_N_DD, 0); p(S_N_TXN, 0); p(S_N_PAR, 0);
+    p(S_N_FR, 1);
+    p(S_N_ITEMS, 0);
+    p(S_CAP_NEED, 0);
+    p(S_N_ENTRIES, 0);
     w.zero_leaf(leafp(0), L);
-    w.st(dl, 0u);
-    w.st(dv, 0u);
-    w.st(sol, 0u);
-    w.st(fr, ROOT_ORDER);
+    w.st(dl(), 0u);
+    w.st(dv(), 0u);
+    w.st(sol(), 0u);
+    w.st(fr(), ROOT_ORDER);
     w.root_init(0u, 1u, 0u);
   }
   CRDT_HD void begin() {
-    w.root_load(groups, s.ng);
-    if (s.n_cwo) cwo_last = w.ld_cwo(cwo + s.n_cwo - 1);
-    if (s.n_del) del_last = w.ld_del(dels + s.n_del - 1);
-    if (s.n_txn) {
-      TxnRec t = w.ld_txn(txns + s.n_txn - 1);
-      tx_order = t.order;
-      tx_len = t.len;
-      tx_shadow = t.shadow;
+    w.root_load(groups(), g(S_NG));
+    u32 n = g(S_N_CWO);
+    if (n) {
+      CwoRun r = w.ld_cwo(cwo() + n - 1);
+      p(T_CWO_KEY, r.key); p(T_CWO_AGENT, r.agent); p(T_CWO_SEQ, r.seq); p(T_CWO_LEN, r.len);
     }
-    fr0 = w.ld(fr);
+    n = g(S_N_DEL);
+    if (n) {
+      DelRun r = w.ld_del(dels() + n - 1);
+      p(T_DEL_KEY, r.key); p(T_DEL_ORDER, r.order); p(T_DEL_LEN, r.len);
+    }
+    n = g(S_N_TXN);
+    if (n) {
+      TxnRec t = w.ld_txn(txns() + n - 1);
+      p(T_TX_ORDER, t.order); p(T_TX_LEN, t.len); p(T_TX_SHADOW, t.shadow);
+    }
+    p(T_FR0, w.ld(fr()));
   }
   CRDT_HD void finish() {
     commit();
-    w.root_store(groups, s.ng);
-    w.st_state(stp, s);
+    w.root_store(groups(), g(S_NG));
+    w.x_store_state(stp(), S_BASE);
   }
 
   // ------------------------------------------------------------------ records
   CRDT_HD Rec rec(u32 pos) {
-    if (pos - rb_base >= 64u) {
-      rb_base = pos;
-      u32 n = rec_n - pos;
-      w.rec_block_load(recs + pos, n < 64u ? n : 64u);
+    u32 rb = g(T_RB_BASE);
+    if (pos - rb >= 64u) {
+      rb = pos;
+      p(T_RB_BASE, pos);
+      u32 n = rec_n() - pos;
+      w.rec_block_load(recs() + pos, n < 64u ? n : 64u);
     }
-    return w.rec_get(pos - rb_base);
+    return w.rec_get(pos - rb);
   }
 
   // ------------------------------------------------------------------ directory
   CRDT_HD void slot_of(u32 leaf, u32& blk, u32& i) const {
-    if (leaf == c_leaf) { blk = c_blk; i = c_i; return; }
-    u32 v = w.ld(sol + leaf);
+    if (leaf == g(C_LEAF)) { blk = g(C_BLK); i = g(C_I); return; }
+    u32 v = w.ld(sol() + leaf);
     blk = v >> 6;
     i = v & 63u;
   }
   CRDT_HD u32 pos_key(u32 leaf) const {  // total order of leaves in the document
     u32 blk, i;
     slot_of(leaf, blk, i);
-    return (w.root_find_blk(s.ng, blk) << 6) | i;
+    return (w.root_find_blk(g(S_NG), blk) << 6) | i;
   }
   CRDT_HD u32 leaf_at_start() const { return w.ld(dleaf(w.root_blk(0))); }
   CRDT_HD u32 leaf_at_end() const {
-    u32 g = s.ng - 1;
-    return w.ld(dleaf(w.root_blk(g)) + w.root_cnt(g) - 1);
+    u32 gg = g(S_NG) - 1;
+    return w.ld(dleaf(w.root_blk(gg)) + w.root_cnt(gg) - 1);
   }
   CRDT_HD u32 next_leaf(u32 leaf) const {
     u32 blk, i;
     slot_of(leaf, blk, i);
-    u32 g = w.root_find_blk(s.ng, blk);
-    if (i + 1 < w.root_cnt(g)) return w.ld(dleaf(blk) + i + 1);
-    if (g + 1 < s.ng) return w.ld(dleaf(w.root_blk(g + 1)));
+    u32 gg = w.root_find_blk(g(S_NG), blk);
+    if (i + 1 < w.root_cnt(gg)) return w.ld(dleaf(blk) + i + 1);
+    if (gg + 1 < g(S_NG)) return w.ld(dleaf(w.root_blk(gg + 1)));
     return INVALID;
   }
   // Record the cached leaf's new visible count in the directory.
   CRDT_HD void dir_set_cached_vis(u32 v) {
-    if (v == c_vis) return;
-    w.st(dvis(c_blk) + c_i, v);
-    w.root_add_vis(w.root_find_blk(s.ng, c_blk), v - c_vis);
-    s.len += v - c_vis;
-    c_vis = v;
+    u32 old = g(C_VIS);
+    if (v == old) return;
+    u32 blk = g(C_BLK);
+    w.st(dvis(blk) + g(C_I), v);
+    w.root_add_vis(w.root_find_blk(g(S_NG), blk), v - old);
+    inc(S_LEN, v - old);
+    p(C_VIS, v);
   }
   // First leaf whose visible range contains `pos` (root.rs:54-88 descent, ContentIndex).
   CRDT_HD bool find_by_pos(u32 pos, u32& leaf, u32& vstart, u32& blk, u32& i) const {
-    u32 g, base;
-    if (!w.root_find_pos(s.ng, pos, g, base)) return false;
-    blk = w.root_blk(g);
+    u32 gg, base;
+    if (!w.root_find_pos(g(S_NG), pos, gg, base)) return false;
+    blk = w.root_blk(gg);
     u32 before;
-    if (!w.blk_find_pos(dvis(blk), dleaf(blk), w.root_cnt(g), pos - base, i, before, leaf)) return false;
+    if (!w.blk_find_pos(dvis(blk), dleaf(blk), w.root_cnt(gg), pos - base, i, before, leaf)) return false;
     vstart = base + before;
     return true;
   }
 
   // ------------------------------------------------------------------ leaf cache
   CRDT_HD void commit() {
-    if (c_leaf == INVALID || !c_dirty) return;
-    w.cache_store(leafp(c_leaf));
-    dir_set_cached_vis(c_now);
-    c_dirty = false;
+    u32 lf = g(C_LEAF);
+    if (lf == INVALID || !g(C_DIRTY)) return;
+    w.cache_store(leafp(lf));
+    dir_set_cached_vis(g(C_NOW));
+    p(C_DIRTY, 0);
   }
   CRDT_HD void load_cache(u32 leaf, u32 blk, u32 i) {
     commit();
-    c_n = w.cache_load(leafp(leaf));
-    c_leaf = leaf;
-    c_blk = blk;
-    c_i = i;
-    c_dirty = false;
-    c_now = c_vis = w.cache_vis_from(0u);
-    c_vs_ok = false;
+    p(C_N, w.cache_load(leafp(leaf)));
+    p(C_LEAF, leaf);
+    p(C_BLK, blk);
+    p(C_I, i);
+    p(C_DIRTY, 0);
+    u32 v = w.cache_vis_from(0u);
+    p(C_NOW, v);
+    p(C_VIS, v);
+    p(C_VS_OK, 0);
   }
   CRDT_HD void ensure(u32 leaf) {
-    if (leaf == c_leaf) return;
-    u32 v = w.ld(sol + leaf);
+    if (leaf == g(C_LEAF)) return;
+    u32 v = w.ld(sol() + leaf);
     load_cache(leaf, v >> 6, v & 63u);
   }
   // set entry idx of the cached leaf (tracks the cached visible count exactly)
   CRDT_HD void set(u32 idx, const Span& e) {
-    c_now = c_now - clen_i(w.cget_len(idx)) + clen(e);
+    p(C_NOW, g(C_NOW) - clen_i(w.cget_len(idx)) + clen(e));
     w.cset(idx, e);
-    c_dirty = true;
+    p(C_DIRTY, 1);
   }
   CRDT_HD static u32 clen_i(i32 len) { return len > 0 ? (u32)len : 0u; }
   CRDT_HD static u32 slen_i(i32 len) { return (u32)(len < 0 ? -len : len); }
-  CRDT_HD u32 cur_len() const { return s.len + c_now - c_vis; }
+  CRDT_HD u32 cur_len() const { return g(S_LEN) + g(C_NOW) - g(C_VIS); }
 
   // ------------------------------------------------------------------ order -> leaf map
   // ListCRDT::notify (doc.rs:143-153): all orders of `e` now live in `leaf`.  `home` is the
   // leaf the run already lives in (INVALID for freshly inserted orders): no write if unchanged.
   CRDT_HD void notify(const Span& e, u32 leaf, u32 home) {
     if (home == leaf) return;
-    w.fill(lof + e.order, slen(e), leaf);
+    w.fill(lof() + e.order, slen(e), leaf);
   }
 
   // ------------------------------------------------------------------ cursor ops
   // cursor.rs:127-145 (next_entry) / cursor.rs:26-103 (traverse).  Moves the cache along.
   CRDT_HD bool next_entry(Cursor& c) {
     ensure(c.leaf);
-    if (c.idx + 1 < c_n) { c.idx++; c.off = 0; return true; }
+    if (c.idx + 1 < g(C_N)) { c.idx++; c.off = 0; return true; }
     u32 nl = next_leaf(c.leaf);
     if (nl == INVALID) return false;
     c.leaf = nl;
@@ -267,7 +315,7 @@ struct Replayer {
     if (c.off == slen_i(w.cget_len(c.idx))) {
       c.off = 0;
       c.idx++;
-      if (c.idx >= c_n) return next_entry(c);
+      if (c.idx >= g(C_N)) return next_entry(c);
     }
     return true;
   }
@@ -279,7 +327,7 @@ struct Replayer {
     if (off == slen_i(w.cget_len(idx))) {
       off = 0;
       idx++;
-      if (idx >= c_n) {
+      if (idx >= g(C_N)) {
         u32 nl = next_leaf(c.leaf);
         if (nl == INVALID) return false;
         out = w.ld(&leafp(nl)->order);
@@ -301,17 +349,18 @@ struct Replayer {
   CRDT_HD Cursor cursor_at_start() const { return Cursor{leaf_at_start(), 0, 0}; }  // root.rs:133-150
   // root.rs:54-88 + 401-411, leaf.rs:61-84 (stick_end = false)
   CRDT_HD bool cursor_at_content_pos(u32 pos, Cursor& c) {
-    if (!(c_leaf != INVALID && c_vs_ok && pos >= c_vstart && pos < c_vstart + c_now)) {
+    u32 vs = g(C_VSTART);
+    if (!(g(C_LEAF) != INVALID && g(C_VS_OK) && pos >= vs && pos < vs + g(C_NOW))) {
       commit();
-      u32 lf, vs, blk, i;
+      u32 lf, blk, i;
       if (!find_by_pos(pos, lf, vs, blk, i)) return false;
-      if (lf != c_leaf) load_cache(lf, blk, i);
-      c_vstart = vs;
-      c_vs_ok = true;
+      if (lf != g(C_LEAF)) load_cache(lf, blk, i);
+      p(C_VSTART, vs);
+      p(C_VS_OK, 1);
     }
     u32 idx, off;
-    if (!w.cfind_content(c_n, pos - c_vstart, idx, off)) return false;
-    c = Cursor{c_leaf, idx, off};
+    if (!w.cfind_content(g(C_N), pos - vs, idx, off)) return false;
+    c = Cursor{g(C_LEAF), idx, off};
     return true;
   }
   // doc.rs:101-136 (marker_at + cursor_before_item, leaf.rs:41-57).  `load`: move the cache to
@@ -320,21 +369,23 @@ struct Replayer {
     if (order == ROOT_ORDER) {  // root.rs:90-123 cursor_at_end
       u32 lf = leaf_at_end();
       ensure(lf);
-      if (c_n == 0) return false;
-      c = Cursor{lf, c_n - 1, slen_i(w.cget_len(c_n - 1))};
+      u32 n = g(C_N);
+      if (n == 0) return false;
+      c = Cursor{lf, n - 1, slen_i(w.cget_len(n - 1))};
       return true;
     }
-    if (order >= s.next_order) return false;
-    i32 idx = c_leaf != INVALID ? w.cfind_order(c_n, order) : -1;  // cached leaf first: no load
+    if (order >= g(S_NEXT_ORDER)) return false;
+    u32 cl = g(C_LEAF);
+    i32 idx = cl != INVALID ? w.cfind_order(g(C_N), order) : -1;  // cached leaf first: no load
     if (idx >= 0) {
-      c = Cursor{c_leaf, (u32)idx, order - w.cget_order((u32)idx)};
+      c = Cursor{cl, (u32)idx, order - w.cget_order((u32)idx)};
       return true;
     }
-    u32 lf = w.ld(lof + order);
-    if (lf == INVALID || lf == c_leaf) return false;
+    u32 lf = w.ld(lof() + order);
+    if (lf == INVALID || lf == cl) return false;
     if (load) {
       ensure(lf);
-      idx = w.cfind_order(c_n, order);
+      idx = w.cfind_order(g(C_N), order);
       if (idx < 0) return false;
       c = Cursor{lf, (u32)idx, order - w.cget_order((u32)idx)};
       return true;
@@ -361,35 +412,40 @@ struct Replayer {
   // mutations.rs:623-669 split_at: [idx, n) of the cached leaf moves to a new leaf (after
   // `padding` empty slots), which is linked right after the cached leaf.  Returns its id.
   CRDT_HD u32 split_at(u32 idx, u32 padding) {
-    u32 nl = s.n_leaves++;
+    u32 nl = g(S_N_LEAVES);
+    p(S_N_LEAVES, nl + 1);
+    u32 n = g(C_N);
     u32 stolen = w.cache_vis_from(idx);
-    w.cache_write_moved(leafp(nl), idx, c_n, padding);
-    for (u64 m = w.lanes_in(idx, c_n); m; m &= m - 1) {  // notify every moved entry
+    w.cache_write_moved(leafp(nl), idx, n, padding);
+    for (u64 m = w.lanes_in(idx, n); m; m &= m - 1) {  // notify every moved entry
       Span e = w.cget(w.first_lane(m));
-      w.fill(lof + e.order, slen(e), nl);
+      w.fill(lof() + e.order, slen(e), nl);
     }
-    w.cache_clear(idx, c_n);
-    c_now -= stolen;
-    c_n = idx;
-    c_dirty = true;
+    w.cache_clear(idx, n);
+    p(C_NOW, g(C_NOW) - stolen);
+    p(C_N, idx);
+    p(C_DIRTY, 1);
     // link nl right after the cached leaf (directory block insert; the block splits when full)
-    u32 blk = c_blk, i = c_i;
-    u32 g = w.root_find_blk(s.ng, blk);
-    u32 cnt = w.root_cnt(g);
-    if (cnt == GROUP) {  // split the block: [32, 64) -> new block in group g+1
-      u32 nb = s.n_blocks++;
-      u32 mv = w.blk_split(dleaf(blk), dvis(blk), dleaf(nb), dvis(nb), sol, nb);
-      w.root_set(g, blk, 32u, w.root_vis(g) - mv);
-      w.root_insert(s.ng, g + 1, nb, 32u, mv);
-      s.ng++;
-      if (i >= 32) { blk = nb; i -= 32; g = g + 1; c_blk = nb; c_i = i; }
+    u32 blk = g(C_BLK), i = g(C_I);
+    u32 ng = g(S_NG);
+    u32 gg = w.root_find_blk(ng, blk);
+    u32 cnt = w.root_cnt(gg);
+    if (cnt == GROUP) {  // split the block: [32, 64) -> new block in group gg+1
+      u32 nb = g(S_N_BLOCKS);
+      p(S_N_BLOCKS, nb + 1);
+      u32 mv = w.blk_split(dleaf(blk), dvis(blk), dleaf(nb), dvis(nb), sol(), nb);
+      w.root_set(gg, blk, 32u, w.root_vis(gg) - mv);
+      w.root_insert(ng, gg + 1, nb, 32u, mv);
+      p(S_NG, ng + 1);
+      if (i >= 32) { blk = nb; i -= 32; gg = gg + 1; p(C_BLK, nb); p(C_I, i); }
       cnt = 32;
     }
-    w.blk_insert(dleaf(blk), dvis(blk), cnt, i + 1, nl, stolen, sol, blk);
+    w.blk_insert(dleaf(blk), dvis(blk), cnt, i + 1, nl, stolen, sol(), blk);
     // the cached leaf's directory count loses `stolen` (moved to nl); group total unchanged
-    w.root_set(g, blk, cnt + 1, w.root_vis(g));
-    w.st(dvis(c_blk) + c_i, c_vis - stolen);
-    c_vis -= stolen;
+    w.root_set(gg, blk, cnt + 1, w.root_vis(gg));
+    u32 cv = g(C_VIS) - stolen;
+    w.st(dvis(blk) + i, cv);
+    p(C_VIS, cv);
     return nl;
   }
   // mutations.rs:17-179 insert_internal.  Items a0..a(n-1) (n <= 3) stay in named registers;
@@ -424,7 +480,7 @@ struct Replayer {
       if (n == 0 && !has_rem) return true;
       c.off = 0;
       c.idx += 1;
-      if (!has_rem && c.idx < c_n) {  // prepend the tail of the items onto the next entry
+      if (!has_rem && c.idx < g(C_N)) {  // prepend the tail of the items onto the next entry
         Span nx = w.cget(c.idx);
         bool pre = false;
         while (true) {
@@ -443,25 +499,26 @@ struct Replayer {
     }
     u32 space = n + (has_rem ? 1u : 0u);
     if (space > (u32)L / 2) return false;  // mutations.rs:121 assert
-    s.n_entries += space;
+    inc(S_N_ENTRIES, space);
     bool rem_moved = false;
-    if (c_n + space > (u32)L) {
+    u32 cn = g(C_N);
+    if (cn + space > (u32)L) {
       bool follow = c.idx >= (u32)L / 2;
-      u32 moved = c_n - c.idx;
+      u32 moved = cn - c.idx;
       u32 nl = split_at(c.idx, follow ? space : 0u);
       if (follow) {  // the cursor follows the new leaf; its first `space` slots are padding
         commit();
         ensure(nl);
-        c_n = space + moved;
+        p(C_N, space + moved);
         c.leaf = nl;
         c.idx = 0;
         rem_moved = true;
       } else {
-        c_n += space;
+        p(C_N, g(C_N) + space);  // split_at left idx entries
       }
     } else {
-      w.cache_shift_right(c.idx, c_n, space);
-      c_n += space;
+      w.cache_shift_right(c.idx, cn, space);
+      p(C_N, cn + space);
     }
     notify(a0, c.leaf, home);
     set(c.idx, a0);
@@ -479,99 +536,113 @@ struct Replayer {
 
   // ------------------------------------------------------------------ RLE side tables
   CRDT_HD void use_agent(u32 a) {  // agent cache (author of the current txn)
-    if (a == ag_id) return;
-    ag_id = a;
-    AgentRec r = w.ld_agent(agents + a);
-    ag_base = r.run_base;
-    ag_cnt = r.run_cnt;
-    ag_cap = r.run_cap;
-    if (ag_cnt) ag_last = w.ld_arun(arun + ag_base + ag_cnt - 1);
+    if (a == g(T_AG_ID)) return;
+    p(T_AG_ID, a);
+    AgentRec r = w.ld_agent(agents() + a);
+    p(T_AG_BASE, r.run_base);
+    p(T_AG_CNT, r.run_cnt);
+    p(T_AG_CAP, r.run_cap);
+    if (r.run_cnt) {
+      ARun x = w.ld_arun(arun() + r.run_base + r.run_cnt - 1);
+      p(T_AGL_KEY, x.key); p(T_AGL_ORDER, x.order); p(T_AGL_LEN, x.len);
+    }
   }
   CRDT_HD u32 agent_next_seq(u32 agent) {  // doc.rs:20-24
     use_agent(agent);
-    return ag_cnt ? ag_last.key + ag_last.len : 0u;
+    return g(T_AG_CNT) ? g(T_AGL_KEY) + g(T_AGL_LEN) : 0u;
   }
   CRDT_HD bool seq_to_order(u32 agent, u32 seq, u32& order) const {  // doc.rs:26-29
     u32 base, cnt;
-    if (agent == ag_id) {
-      if (ag_cnt && seq >= ag_last.key && seq - ag_last.key < ag_last.len) {
-        order = ag_last.order + (seq - ag_last.key);
+    if (agent == g(T_AG_ID)) {
+      u32 key = g(T_AGL_KEY);
+      if (g(T_AG_CNT) && seq >= key && seq - key < g(T_AGL_LEN)) {
+        order = g(T_AGL_ORDER) + (seq - key);
         return true;
       }
-      base = ag_base;
-      cnt = ag_cnt;
+      base = g(T_AG_BASE);
+      cnt = g(T_AG_CNT);
     } else {
-      AgentRec A = w.ld_agent(agents + agent);
+      AgentRec A = w.ld_agent(agents() + agent);
       base = A.run_base;
       cnt = A.run_cnt;
     }
-    i32 k = w.search_arun(arun + base, cnt, seq);
+    ARun* ar = arun() + base;
+    i32 k = w.search_arun(ar, cnt, seq);
     if (k < 0) return false;
-    ARun r = w.ld_arun(arun + base + k);
+    ARun r = w.ld_arun(ar + k);
     order = r.order + (seq - r.key);
     return true;
   }
   CRDT_HD bool order_to_agent(u32 order, u32& agent) const {  // client_with_order.get()
-    if (s.n_cwo && order >= cwo_last.key && order - cwo_last.key < cwo_last.len) { agent = cwo_last.agent; return true; }
-    i32 k = w.search_cwo(cwo, s.n_cwo, order);
+    u32 n = g(S_N_CWO), key = g(T_CWO_KEY);
+    if (n && order >= key && order - key < g(T_CWO_LEN)) { agent = g(T_CWO_AGENT); return true; }
+    i32 k = w.search_cwo(cwo(), n, order);
     if (k < 0) return false;
-    agent = w.ld_cwo(cwo + k).agent;
+    agent = w.ld_cwo(cwo() + k).agent;
     return true;
   }
   // doc.rs:155-165 assign_order_to_client
   CRDT_HD void assign_order_to_client(u32 agent, u32 seq, u32 order, u32 len) {
-    if (s.n_cwo > 0 && order == cwo_last.key + cwo_last.len && agent == cwo_last.agent && seq == cwo_last.seq + cwo_last.len) {
-      cwo_last.len += len;
-      w.st(&cwo[s.n_cwo - 1].len, cwo_last.len);
+    u32 n = g(S_N_CWO);
+    u32 ck = g(T_CWO_KEY), cl = g(T_CWO_LEN);
+    if (n > 0 && order == ck + cl && agent == g(T_CWO_AGENT) && seq == g(T_CWO_SEQ) + cl) {
+      p(T_CWO_LEN, cl + len);
+      w.st(&cwo()[n - 1].len, cl + len);
     } else {
-      cwo_last = CwoRun{order, agent, seq, len};
-      w.st_cwo(cwo + s.n_cwo, cwo_last);
-      s.n_cwo++;
+      p(T_CWO_KEY, order); p(T_CWO_AGENT, agent); p(T_CWO_SEQ, seq); p(T_CWO_LEN, len);
+      w.st_cwo(cwo() + n, CwoRun{order, agent, seq, len});
+      p(S_N_CWO, n + 1);
     }
     use_agent(agent);
-    if (ag_cnt > 0 && seq == ag_last.key + ag_last.len && order == ag_last.order + ag_last.len) {
-      ag_last.len += len;
-      w.st(&arun[ag_base + ag_cnt - 1].len, ag_last.len);
+    u32 an = g(T_AG_CNT), base = g(T_AG_BASE);
+    u32 lk = g(T_AGL_KEY), ll = g(T_AGL_LEN);
+    if (an > 0 && seq == lk + ll && order == g(T_AGL_ORDER) + ll) {
+      p(T_AGL_LEN, ll + len);
+      w.st(&arun()[base + an - 1].len, ll + len);
     } else {
-      ag_last = ARun{seq, order, len, 0};
-      w.st_arun(arun + ag_base + ag_cnt, ag_last);
-      ag_cnt++;
-      w.st(&agents[agent].run_cnt, ag_cnt);
+      p(T_AGL_KEY, seq); p(T_AGL_ORDER, order); p(T_AGL_LEN, len);
+      w.st_arun(arun() + base + an, ARun{seq, order, len, 0});
+      p(T_AG_CNT, an + 1);
+      w.st(&agents()[agent].run_cnt, an + 1);
     }
   }
   CRDT_HD void append_delete(u32 key, u32 target, u32 len) {  // Rle<KVPair<DeleteEntry>>::append
-    if (s.n_del > 0 && key == del_last.key + del_last.len && del_last.order + del_last.len == target) {
-      del_last.len += len;
-      w.st(&dels[s.n_del - 1].len, del_last.len);
+    u32 n = g(S_N_DEL);
+    u32 dk = g(T_DEL_KEY), dlen = g(T_DEL_LEN);
+    if (n > 0 && key == dk + dlen && g(T_DEL_ORDER) + dlen == target) {
+      p(T_DEL_LEN, dlen + len);
+      w.st(&dels()[n - 1].len, dlen + len);
       return;
     }
-    del_last = DelRun{key, target, len};
-    w.st_del(dels + s.n_del, del_last);
-    s.n_del++;
+    p(T_DEL_KEY, key); p(T_DEL_ORDER, target); p(T_DEL_LEN, len);
+    w.st_del(dels() + n, DelRun{key, target, len});
+    p(S_N_DEL, n + 1);
   }
   // double_delete.rs:41-107 increment_delete_range (rare path; scalar)
   CRDT_HD bool dd_insert_at(u32 idx, DDRun r) {
-    if (s.n_dd + 1 > cap_dd) return false;
-    for (u32 k = s.n_dd; k > idx; k--) w.st_dd(dd + k, w.ld_dd(dd + k - 1));
-    w.st_dd(dd + idx, r);
-    s.n_dd++;
+    u32 n = g(S_N_DD);
+    if (n + 1 > g(K_DD)) return false;
+    DDRun* b = dd();
+    for (u32 k = n; k > idx; k--) w.st_dd(b + k, w.ld_dd(b + k - 1));
+    w.st_dd(b + idx, r);
+    p(S_N_DD, n + 1);
     return true;
   }
   CRDT_HD bool increment_delete_range(u32 base, u32 len) {
-    DDRun* b = dd;
+    DDRun* b = dd();
     DDRun next{base, len, 1};
-    i32 k = w.search_dd(b, s.n_dd, base);
+    i32 k = w.search_dd(b, g(S_N_DD), base);
     u32 idx;
     if (k >= 0) idx = (u32)k;
     else {  // insertion point: first entry with key > base
       idx = 0;
-      while (idx < s.n_dd && w.ld_dd(b + idx).key <= base) idx++;
+      while (idx < g(S_N_DD) && w.ld_dd(b + idx).key <= base) idx++;
     }
     while (true) {
-      if (idx == s.n_dd || w.ld_dd(b + idx).key > next.key) {
+      if (idx == g(S_N_DD) || w.ld_dd(b + idx).key > next.key) {
         DDRun here = next;
         bool done_here;
-        if (idx < s.n_dd && next.key + next.len > w.ld_dd(b + idx).key) {
+        if (idx < g(S_N_DD) && next.key + next.len > w.ld_dd(b + idx).key) {
           u32 at = w.ld_dd(b + idx).key - here.key;
           next = DDRun{here.key + at, here.len - at, here.excess};
           here.len = at;
@@ -579,8 +650,8 @@ struct Replayer {
         } else done_here = true;
         bool app = false;
         if (idx >= 1) {
-          DDRun p = w.ld_dd(b + idx - 1);
-          if (here.key == p.key + p.len && here.excess == p.excess) { w.st(&b[idx - 1].len, p.len + here.len); app = true; }
+          DDRun q = w.ld_dd(b + idx - 1);
+          if (here.key == q.key + q.len && here.excess == q.excess) { w.st(&b[idx - 1].len, q.len + here.len); app = true; }
         }
         if (!app) { if (!dd_insert_at(idx, here)) return false; idx++; }
         if (done_here) break;
@@ -609,68 +680,74 @@ struct Replayer {
     }
     return true;
   }
-  CRDT_HD bool par_contains(const u32* p, u32 np, u32 p0, u32 x) const {
+  CRDT_HD bool par_contains(const u32* pp, u32 np, u32 p0, u32 x) const {
     if (np == 0) return false;
     if (p0 == x) return true;
-    for (u32 j = 1; j < np; j++) if (w.ld(p + j) == x) return true;
+    for (u32 j = 1; j < np; j++) if (w.ld(pp + j) == x) return true;
     return false;
   }
   // doc.rs:350-374 insert_txn (+ advance_branch_by :34-48).  Remote parents are already in the
   // pool at [n_par, n_par + np), the first one also in p0.
   CRDT_HD i32 insert_txn(bool remote, u32 first, u32 len, u32 np, u32 p0) {
-    u32* pp = par + s.n_par;
+    u32 npar = g(S_N_PAR);
+    u32* pp = par() + npar;
+    u32* f = fr();
     u32 last = first + len - 1;
+    u32 nfr = g(S_N_FR);
+    u32 f0 = g(T_FR0);
     if (remote) {
-      if (s.n_fr == 1) {
-        if (fr0 == first) return ST_FRONTIER;
-        if (par_contains(pp, np, p0, fr0)) { fr0 = last; w.st(fr, last); }
-        else { w.st(fr + 1, last); s.n_fr = 2; }
+      if (nfr == 1) {
+        if (f0 == first) return ST_FRONTIER;
+        if (par_contains(pp, np, p0, f0)) { p(T_FR0, last); w.st(f, last); }
+        else { w.st(f + 1, last); p(S_N_FR, 2); }
       } else {
-        for (u32 k = 0; k < s.n_fr; k++) if (w.ld(fr + k) == first) return ST_FRONTIER;
+        for (u32 k = 0; k < nfr; k++) if (w.ld(f + k) == first) return ST_FRONTIER;
         u32 m = 0;
-        for (u32 k = 0; k < s.n_fr; k++) {
-          u32 o = w.ld(fr + k);
-          if (!par_contains(pp, np, p0, o)) { w.st(fr + m, o); m++; }
+        for (u32 k = 0; k < nfr; k++) {
+          u32 o = w.ld(f + k);
+          if (!par_contains(pp, np, p0, o)) { w.st(f + m, o); m++; }
         }
         if (m + 1 > FRONTIER_CAP) return ST_CAPACITY;
-        w.st(fr + m, last);
-        s.n_fr = m + 1;
-        fr0 = w.ld(fr);
+        w.st(f + m, last);
+        p(S_N_FR, m + 1);
+        p(T_FR0, w.ld(f));
       }
     } else {
-      np = s.n_fr;
-      p0 = fr0;
-      w.st(pp, fr0);
-      for (u32 k = 1; k < np; k++) w.st(pp + k, w.ld(fr + k));
-      w.st(fr, last);
-      fr0 = last;
-      s.n_fr = 1;
+      np = nfr;
+      p0 = f0;
+      w.st(pp, f0);
+      for (u32 k = 1; k < np; k++) w.st(pp + k, w.ld(f + k));
+      w.st(f, last);
+      p(T_FR0, last);
+      p(S_N_FR, 1);
     }
+    u32 ntx = g(S_N_TXN);
+    u32 txo = g(T_TX_ORDER), txl = g(T_TX_LEN), txs = g(T_TX_SHADOW);
     u32 shadow = first;
     while (shadow >= 1 && par_contains(pp, np, p0, shadow - 1)) {
       u32 x = shadow - 1;
-      if (s.n_txn && x >= tx_order && x - tx_order < tx_len) { shadow = tx_shadow; continue; }
-      i32 k = w.search_txn(txns, s.n_txn, x);
+      if (ntx && x >= txo && x - txo < txl) { shadow = txs; continue; }
+      i32 k = w.search_txn(txns(), ntx, x);
       if (k < 0) return ST_UNKNOWN_ID;
-      shadow = w.ld(&txns[k].shadow);
+      shadow = w.ld(&txns()[k].shadow);
     }
-    if (s.n_txn > 0 && np == 1 && p0 == tx_order + tx_len - 1 && shadow == tx_shadow) {
-      tx_len += len;
-      w.st(&txns[s.n_txn - 1].len, tx_len);
+    if (ntx > 0 && np == 1 && p0 == txo + txl - 1 && shadow == txs) {
+      p(T_TX_LEN, txl + len);
+      w.st(&txns()[ntx - 1].len, txl + len);
       return ST_OK;  // parents of a merged txn are not kept
     }
-    tx_order = first;
-    tx_len = len;
-    tx_shadow = shadow;
-    w.st_txn(txns + s.n_txn, TxnRec{first, len, shadow, s.n_par, np, {0, 0, 0}});
-    s.n_txn++;
-    s.n_par += np;
+    p(T_TX_ORDER, first);
+    p(T_TX_LEN, len);
+    p(T_TX_SHADOW, shadow);
+    w.st_txn(txns() + ntx, TxnRec{first, len, shadow, npar, np, {0, 0, 0}});
+    p(S_N_TXN, ntx + 1);
+    p(S_N_PAR, npar + np);
     return ST_OK;
   }
 
   CRDT_HD i32 id_to_order(u32 agent, u32 seq, u32& order) const {  // doc.rs:236-240
     if (agent == ROOT_AGENT) { order = ROOT_ORDER; return ST_OK; }
-    if (agent >= s.n_agents) return ST_UNKNOWN_AGENT;
+    if (agent >= g(S_N_AGENTS)) return ST_UNKNOWN_AGENT;
     if (!seq_to_order(agent, seq, order)) return ST_UNKNOWN_ID;
     return ST_OK;
   }
@@ -679,17 +756,17 @@ struct Replayer {
   // Capacity needed by a txn (checked before any mutation, so a capacity stop is resumable at
   // this txn).  Every block but the first holds >= 32 slots, so blk_cap = leaf_cap/32 + 2 and
   // leaf_cap <= 32*(MAX_GROUPS-1) (host-enforced) bound blocks and root groups as well.
-  // On failure s.cap_need records which table (bit) must grow.
+  // On failure S_CAP_NEED records which table (bit) must grow.
   CRDT_HD bool fits(bool remote, u32 agent, u32 n_ops, u32 n_dels, u32 txn_len, u32 n_parents) {
     u32 need = 0;
-    if ((u64)s.n_leaves + 2ull * n_ops > cap_leaf) need |= 1u;
-    if (s.n_cwo + 1 > cap_cwo || s.n_txn + 1 > cap_txn) need |= 2u;
-    if ((u64)s.n_del + n_dels > cap_del) need |= 4u;
-    if ((u64)s.n_par + (remote ? n_parents : s.n_fr) > cap_par) need |= 8u;
-    if ((u64)s.next_order + txn_len > cap_map) need |= 16u;
+    if ((u64)g(S_N_LEAVES) + 2ull * n_ops > g(K_LEAF)) need |= 1u;
+    if (g(S_N_CWO) + 1 > g(K_CWO) || g(S_N_TXN) + 1 > g(K_TXN)) need |= 2u;
+    if ((u64)g(S_N_DEL) + n_dels > g(K_DEL)) need |= 4u;
+    if ((u64)g(S_N_PAR) + (remote ? n_parents : g(S_N_FR)) > g(K_PAR)) need |= 8u;
+    if ((u64)g(S_NEXT_ORDER) + txn_len > g(K_MAP)) need |= 16u;
     use_agent(agent);
-    if (ag_cnt + 1 > ag_cap) need |= 32u;
-    s.cap_need = need;
+    if (g(T_AG_CNT) + 1 > g(T_AG_CAP)) need |= 32u;
+    p(S_CAP_NEED, need);
     return need == 0;
   }
 
@@ -704,7 +781,7 @@ struct Replayer {
       nops = h.w0 & 0x0FFFFFFFu;
       agent = h.w1;
       txn_len = h.w3;
-      if (agent >= s.n_agents) return ST_UNKNOWN_AGENT;
+      if (agent >= g(S_N_AGENTS)) return ST_UNKNOWN_AGENT;
       if (txn_len == 0) return ST_EMPTY_TXN;
       if (!fits(false, agent, nops, h.w2, txn_len, 0)) return ST_NEED_CAPACITY;
       seq = agent_next_seq(agent);
@@ -714,16 +791,16 @@ struct Replayer {
       np = h.w1 >> 16;
       seq = h.w2;
       txn_len = h.w3;
-      if (agent >= s.n_agents) return ST_UNKNOWN_AGENT;
+      if (agent >= g(S_N_AGENTS)) return ST_UNKNOWN_AGENT;
       if (agent_next_seq(agent) != seq) return ST_SEQ;
       if ((h.w0 >> 27) & 1u) return ST_BAD_INPUT;
       if (txn_len == 0) return ST_EMPTY_TXN;
       if (!fits(true, agent, nops, nops, txn_len, np)) return ST_NEED_CAPACITY;
     }
-    u32 first = s.next_order;
+    u32 first = g(S_NEXT_ORDER);
     u32 next = first;
     assign_order_to_client(agent, seq, first, txn_len);
-    s.next_order = first + txn_len;
+    p(S_NEXT_ORDER, first + txn_len);
 
     u32 k = 0;
     u32 mode = M_FETCH;
@@ -743,8 +820,8 @@ struct Replayer {
           if (del > 0) {
             if ((u64)lpos + del > cur_len()) return ST_POS_OOB;
             if (!cursor_at_content_pos(lpos, c)) return ST_POS_OOB;
-            w.fill(lof + next, del, INVALID);  // delete orders name no item
-            roll(c);                           // mutations.rs:539
+            w.fill(lof() + next, del, INVALID);  // delete orders name no item
+            roll(c);                             // mutations.rs:539
             remaining = del;
             mode = M_LDEL;
           } else if (lins > 0) {
@@ -769,7 +846,7 @@ struct Replayer {
             i32 st = id_to_order(op.w1 & 0xFFFFu, op.w2, target);
             if (st != ST_OK) return st;
             append_delete(next, target, len);  // doc.rs:305-308
-            w.fill(lof + next, len, INVALID);
+            w.fill(lof() + next, len, INVALID);
             next += len;
             remaining = len;
             mode = M_RDEL;
@@ -817,8 +894,8 @@ struct Replayer {
           if (r == 0) {
             u32 oa;
             if (!order_to_agent(oe.order, oa)) return ST_UNKNOWN_ID;
-            u32 my_rank = w.ld(&agents[agent].rank);
-            u32 other_rank = w.ld(&agents[oa].rank);
+            u32 my_rank = w.ld(&agents()[agent].rank);
+            u32 other_rank = w.ld(&agents()[oa].rank);
             if (my_rank > other_rank) scanning = false;
             else if (item.orr == oe.orr) break;
             else { scanning = true; scan_start = c; }
@@ -828,7 +905,7 @@ struct Replayer {
         if (scanning) c = scan_start;
         a0 = item;
         n = 1;
-        s.n_items += (u32)item.len;
+        inc(S_N_ITEMS, (u32)item.len);
         mode = M_FETCH;
       } else {
         if (mode == M_LDEL) {  // mutations.rs:541-556 local_deactivate
@@ -882,7 +959,7 @@ struct Replayer {
     if (!remote && next != first + txn_len) return ST_BAD_INPUT;
     u32 p0 = 0;
     if (remote) {
-      u32* pp = par + s.n_par;
+      u32* pp = par() + g(S_N_PAR);
       for (u32 j = 0; j < np; j++) {
         Rec pr = rec(pos + 1 + nops + j);
         if (rec_kind(pr) != REC_RPARENT) return ST_BAD_INPUT;
@@ -896,10 +973,11 @@ struct Replayer {
     return insert_txn(remote, first, txn_len, np, p0);
   }
 
-  // Replay this document's record stream from s.rec_pos.
+  // Replay this document's record stream from its rec_pos.
   CRDT_HD void run() {
-    u32 pos = s.rec_pos;
-    while (s.status == ST_OK && pos < rec_n) {
+    u32 pos = g(S_REC_POS);
+    u32 rn = rec_n();
+    while (pos < rn) {
       Rec h = rec(pos);
       u32 kind = rec_kind(h);
       i32 st;
@@ -908,16 +986,16 @@ struct Replayer {
         bool remote = kind == REC_RTXN;
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
         consumed = 1 + nops + (remote ? (h.w1 >> 16) : 0u);
-        st = (pos + consumed <= rec_n) ? apply_txn(h, pos, remote) : ST_BAD_INPUT;
+        st = (pos + consumed <= rn) ? apply_txn(h, pos, remote) : ST_BAD_INPUT;
       } else {
         st = ST_BAD_INPUT;
         consumed = 1;
       }
-      if (st == ST_NEED_CAPACITY) { s.status = st; break; }  // resumable at `pos` after growth
-      if (st != ST_OK) { s.status = st; pos += consumed; break; }
+      if (st == ST_NEED_CAPACITY) { p(S_STATUS, (u32)st); break; }  // resumable at `pos` after growth
+      if (st != ST_OK) { p(S_STATUS, (u32)st); pos += consumed; break; }
       pos += consumed;
     }
-    s.rec_pos = pos;
+    p(S_REC_POS, pos);
   }
 };
 

@@ -31,6 +31,30 @@ __device__ __forceinline__ u32 wave_sum(u32 v) { return rdlane(wave_incl_scan(v)
 
 template <int L>
 struct WaveGPU {
+  // ---------------------------------------------------------------- context registers
+  // Per-document scalar state, one field per lane (replay_core.h slot enum), accessed at
+  // compile-time lane numbers: v_readlane / v_writelane, no memory, no SGPR pressure.
+  u32 x0 = 0, x1 = 0;
+  __device__ __forceinline__ u32 xg(u32 f) const { return f < 64 ? rdlane(x0, f) : rdlane(x1, f - 64); }
+  __device__ __forceinline__ void xs(u32 f, u32 v) {
+    bool me = lane_id() == (f & 63u);
+    if (f < 64) x0 = me ? v : x0;
+    else x1 = me ? v : x1;
+  }
+  // DocState <-> slots [base, base + 20) of x0: one lane-parallel load / store
+  __device__ __forceinline__ void x_load_state(const DocState* p, u32 base) {
+    u32 l = lane_id();
+    const u32* q = (const u32*)p;
+    bool mine = l >= base && l < base + (u32)(sizeof(DocState) / 4);
+    u32 v = mine ? q[l - base] : 0u;
+    x0 = mine ? v : x0;
+  }
+  __device__ __forceinline__ void x_store_state(DocState* p, u32 base) const {
+    u32 l = lane_id();
+    u32* q = (u32*)p;
+    if (l >= base && l < base + (u32)(sizeof(DocState) / 4)) q[l - base] = x0;
+  }
+
   // ---------------------------------------------------------------- leaf cache
   u32 eo = 0, el = 0, er = 0;
   i32 en = 0;
