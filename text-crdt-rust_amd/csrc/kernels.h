@@ -33,7 +33,7 @@ __device__ __forceinline__ WaveGPU<L> wave_with_root(u32 (*s_root)[3 * MAX_GROUP
 
 template <int L>
 __global__ __launch_bounds__(256) void k_init(Pools P, u32 n) {
-  u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
   if (d >= n) return;
   ROOT_LDS;
   Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(s_root));

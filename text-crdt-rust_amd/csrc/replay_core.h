@@ -16,9 +16,12 @@
 //     after the end of a leaf) peek at that leaf without evicting the cached one;
 //   * an order->leaf table (u32 per order) replacing the SplitList, written only when a run
 //     changes leaf (the reference's notify() semantics);
-//   * tails of every RLE table (client_with_order, the author's item_orders, deletes, txns,
-//     frontier) kept on chip and a 64-record prefetch of the op stream, so the common op issues
-//     no dependent HBM load at all (stores are fire-and-forget).
+//   * write-back tails of every RLE table (client_with_order, the author's item_orders,
+//     deletes, txns, frontier[0]) kept on chip (a coalescing append costs no store; the tail is
+//     written when a new run starts and at the end), the cached leaf's successor and its first
+//     order, and a 64-record prefetch of the op stream: the common op issues no dependent HBM
+//     load at all and one store (its order -> leaf entry).  On CDNA4 stores count in vmcnt, so
+//     every store avoided also shortens the next dependent load's wait.
 //
 // Code shape (what makes this fast on CDNA4):
 //   * one op interpreter loop per document in which every heavy routine -- integrate's scan,
@@ -39,6 +42,7 @@ namespace crdt {
 struct Cursor {
   u32 leaf, idx, off;
 };
+constexpr u32 END_LEAF = 0xFFFFFFFEu;  // memoised "no successor leaf"
 
 // Context slots (lane numbers of the two context VGPRs; < 64: first register).
 enum : u32 {
@@ -53,6 +57,7 @@ enum : u32 {
   S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES,
   // leaf cache bookkeeping
   C_LEAF = 64, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
+  C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
   // RLE tails
   T_CWO_KEY, T_CWO_AGENT, T_CWO_SEQ, T_CWO_LEN,
   T_DEL_KEY, T_DEL_ORDER, T_DEL_LEN,
@@ -135,6 +140,8 @@ struct Replayer {
     p(C_VSTART, 0);
     p(C_DIRTY, 0);
     p(C_VS_OK, 0);
+    p(C_SUCC, INVALID);
+    p(C_SUCC_ORD, 0);
     p(T_CWO_KEY, 0); p(T_CWO_AGENT, 0); p(T_CWO_SEQ, 0); p(T_CWO_LEN, 0);
     p(T_DEL_KEY, 0); p(T_DEL_ORDER, 0); p(T_DEL_LEN, 0);
     p(T_TX_ORDER, 0); p(T_TX_LEN, 0); p(T_TX_SHADOW, 0);
@@ -189,8 +196,24 @@ struct Replayer {
     }
     p(T_FR0, w.ld(fr()));
   }
+  // write-back tails -> HBM (the tables' last entries; frontier[0])
+  CRDT_HD void flush_tails() {
+    u32 n = g(S_N_CWO);
+    if (n) w.st(&cwo()[n - 1].len, g(T_CWO_LEN));
+    n = g(S_N_DEL);
+    if (n) w.st(&dels()[n - 1].len, g(T_DEL_LEN));
+    n = g(S_N_TXN);
+    if (n) w.st(&txns()[n - 1].len, g(T_TX_LEN));
+    flush_agent();
+    w.st(fr(), g(T_FR0));
+  }
+  CRDT_HD void flush_agent() {
+    u32 a = g(T_AG_ID), cnt = g(T_AG_CNT);
+    if (a != INVALID && cnt) w.st(&arun()[g(T_AG_BASE) + cnt - 1].len, g(T_AGL_LEN));
+  }
   CRDT_HD void finish() {
     commit();
+    flush_tails();
     w.root_store(groups(), g(S_NG));
     w.x_store_state(stp(), S_BASE);
   }
@@ -272,6 +295,19 @@ struct Replayer {
     p(C_NOW, v);
     p(C_VIS, v);
     p(C_VS_OK, 0);
+    p(C_SUCC, INVALID);
+  }
+  // Successor of the cached leaf (INVALID at the end of the document) and its first order,
+  // memoised: only split_at changes it while the cache stays on one leaf.
+  CRDT_HD u32 cached_succ(u32& first_order) {
+    u32 sc = g(C_SUCC);
+    if (sc != INVALID) { first_order = g(C_SUCC_ORD); return sc == END_LEAF ? INVALID : sc; }
+    u32 nl = next_leaf(g(C_LEAF));
+    u32 fo = nl == INVALID ? 0u : w.ld(&leafp(nl)->order);
+    p(C_SUCC, nl == INVALID ? END_LEAF : nl);
+    p(C_SUCC_ORD, fo);
+    first_order = fo;
+    return nl;
   }
   CRDT_HD void ensure(u32 leaf) {
     if (leaf == g(C_LEAF)) return;
@@ -301,7 +337,8 @@ struct Replayer {
   CRDT_HD bool next_entry(Cursor& c) {
     ensure(c.leaf);
     if (c.idx + 1 < g(C_N)) { c.idx++; c.off = 0; return true; }
-    u32 nl = next_leaf(c.leaf);
+    u32 fo;
+    u32 nl = cached_succ(fo);
     if (nl == INVALID) return false;
     c.leaf = nl;
     c.idx = 0;
@@ -328,9 +365,9 @@ struct Replayer {
       off = 0;
       idx++;
       if (idx >= g(C_N)) {
-        u32 nl = next_leaf(c.leaf);
-        if (nl == INVALID) return false;
-        out = w.ld(&leafp(nl)->order);
+        u32 fo;
+        if (cached_succ(fo) == INVALID) return false;
+        out = fo;
         return true;
       }
     }
@@ -416,6 +453,7 @@ struct Replayer {
     p(S_N_LEAVES, nl + 1);
     u32 n = g(C_N);
     u32 stolen = w.cache_vis_from(idx);
+    u32 first_moved = w.cget_order(idx);
     w.cache_write_moved(leafp(nl), idx, n, padding);
     for (u64 m = w.lanes_in(idx, n); m; m &= m - 1) {  // notify every moved entry
       Span e = w.cget(w.first_lane(m));
@@ -446,6 +484,8 @@ struct Replayer {
     u32 cv = g(C_VIS) - stolen;
     w.st(dvis(blk) + i, cv);
     p(C_VIS, cv);
+    p(C_SUCC, padding ? INVALID : nl);  // (with padding the cursor moves to nl next)
+    p(C_SUCC_ORD, first_moved);
     return nl;
   }
   // mutations.rs:17-179 insert_internal.  Items a0..a(n-1) (n <= 3) stay in named registers;
@@ -537,6 +577,7 @@ struct Replayer {
   // ------------------------------------------------------------------ RLE side tables
   CRDT_HD void use_agent(u32 a) {  // agent cache (author of the current txn)
     if (a == g(T_AG_ID)) return;
+    flush_agent();
     p(T_AG_ID, a);
     AgentRec r = w.ld_agent(agents() + a);
     p(T_AG_BASE, r.run_base);
@@ -587,8 +628,8 @@ struct Replayer {
     u32 ck = g(T_CWO_KEY), cl = g(T_CWO_LEN);
     if (n > 0 && order == ck + cl && agent == g(T_CWO_AGENT) && seq == g(T_CWO_SEQ) + cl) {
       p(T_CWO_LEN, cl + len);
-      w.st(&cwo()[n - 1].len, cl + len);
     } else {
+      if (n) w.st(&cwo()[n - 1].len, cl);  // retire the old tail
       p(T_CWO_KEY, order); p(T_CWO_AGENT, agent); p(T_CWO_SEQ, seq); p(T_CWO_LEN, len);
       w.st_cwo(cwo() + n, CwoRun{order, agent, seq, len});
       p(S_N_CWO, n + 1);
@@ -598,8 +639,8 @@ struct Replayer {
     u32 lk = g(T_AGL_KEY), ll = g(T_AGL_LEN);
     if (an > 0 && seq == lk + ll && order == g(T_AGL_ORDER) + ll) {
       p(T_AGL_LEN, ll + len);
-      w.st(&arun()[base + an - 1].len, ll + len);
     } else {
+      if (an) w.st(&arun()[base + an - 1].len, ll);
       p(T_AGL_KEY, seq); p(T_AGL_ORDER, order); p(T_AGL_LEN, len);
       w.st_arun(arun() + base + an, ARun{seq, order, len, 0});
       p(T_AG_CNT, an + 1);
@@ -611,9 +652,9 @@ struct Replayer {
     u32 dk = g(T_DEL_KEY), dlen = g(T_DEL_LEN);
     if (n > 0 && key == dk + dlen && g(T_DEL_ORDER) + dlen == target) {
       p(T_DEL_LEN, dlen + len);
-      w.st(&dels()[n - 1].len, dlen + len);
       return;
     }
+    if (n) w.st(&dels()[n - 1].len, dlen);
     p(T_DEL_KEY, key); p(T_DEL_ORDER, target); p(T_DEL_LEN, len);
     w.st_del(dels() + n, DelRun{key, target, len});
     p(S_N_DEL, n + 1);
@@ -686,8 +727,10 @@ struct Replayer {
     for (u32 j = 1; j < np; j++) if (w.ld(pp + j) == x) return true;
     return false;
   }
-  // doc.rs:350-374 insert_txn (+ advance_branch_by :34-48).  Remote parents are already in the
-  // pool at [n_par, n_par + np), the first one also in p0.
+  // doc.rs:350-374 insert_txn (+ advance_branch_by :34-48).  Remote parents: np of them, the
+  // first in p0; when np > 1 all of them are already in the pool at [n_par, n_par + np).  A
+  // single parent is written to the pool only if the txn does not coalesce (a merged txn keeps
+  // no parents).  frontier[0] lives in T_FR0 (write-back); frontier[1..] in HBM.
   CRDT_HD i32 insert_txn(bool remote, u32 first, u32 len, u32 np, u32 p0) {
     u32 npar = g(S_N_PAR);
     u32* pp = par() + npar;
@@ -698,26 +741,29 @@ struct Replayer {
     if (remote) {
       if (nfr == 1) {
         if (f0 == first) return ST_FRONTIER;
-        if (par_contains(pp, np, p0, f0)) { p(T_FR0, last); w.st(f, last); }
+        if (par_contains(pp, np, p0, f0)) p(T_FR0, last);
         else { w.st(f + 1, last); p(S_N_FR, 2); }
       } else {
-        for (u32 k = 0; k < nfr; k++) if (w.ld(f + k) == first) return ST_FRONTIER;
-        u32 m = 0;
+        for (u32 k = 0; k < nfr; k++) if ((k == 0 ? f0 : w.ld(f + k)) == first) return ST_FRONTIER;
+        u32 m = 0, nf0 = f0;
         for (u32 k = 0; k < nfr; k++) {
-          u32 o = w.ld(f + k);
-          if (!par_contains(pp, np, p0, o)) { w.st(f + m, o); m++; }
+          u32 o = k == 0 ? f0 : w.ld(f + k);
+          if (!par_contains(pp, np, p0, o)) {
+            if (m == 0) nf0 = o;
+            else w.st(f + m, o);
+            m++;
+          }
         }
         if (m + 1 > FRONTIER_CAP) return ST_CAPACITY;
-        w.st(f + m, last);
+        if (m == 0) nf0 = last;
+        else w.st(f + m, last);
         p(S_N_FR, m + 1);
-        p(T_FR0, w.ld(f));
+        p(T_FR0, nf0);
       }
     } else {
       np = nfr;
       p0 = f0;
-      w.st(pp, f0);
       for (u32 k = 1; k < np; k++) w.st(pp + k, w.ld(f + k));
-      w.st(f, last);
       p(T_FR0, last);
       p(S_N_FR, 1);
     }
@@ -732,10 +778,11 @@ struct Replayer {
       shadow = w.ld(&txns()[k].shadow);
     }
     if (ntx > 0 && np == 1 && p0 == txo + txl - 1 && shadow == txs) {
-      p(T_TX_LEN, txl + len);
-      w.st(&txns()[ntx - 1].len, txl + len);
-      return ST_OK;  // parents of a merged txn are not kept
+      p(T_TX_LEN, txl + len);  // write-back: the merged length reaches HBM with the tail
+      return ST_OK;            // parents of a merged txn are not kept
     }
+    if (np) w.st(pp, p0);
+    if (ntx) w.st(&txns()[ntx - 1].len, txl);  // retire the old tail
     p(T_TX_ORDER, first);
     p(T_TX_LEN, len);
     p(T_TX_SHADOW, shadow);
@@ -758,14 +805,15 @@ struct Replayer {
   // leaf_cap <= 32*(MAX_GROUPS-1) (host-enforced) bound blocks and root groups as well.
   // On failure S_CAP_NEED records which table (bit) must grow.
   CRDT_HD bool fits(bool remote, u32 agent, u32 n_ops, u32 n_dels, u32 txn_len, u32 n_parents) {
+    // room = cap - count (count <= cap always holds), compared in 32 bits
     u32 need = 0;
-    if ((u64)g(S_N_LEAVES) + 2ull * n_ops > g(K_LEAF)) need |= 1u;
-    if (g(S_N_CWO) + 1 > g(K_CWO) || g(S_N_TXN) + 1 > g(K_TXN)) need |= 2u;
-    if ((u64)g(S_N_DEL) + n_dels > g(K_DEL)) need |= 4u;
-    if ((u64)g(S_N_PAR) + (remote ? n_parents : g(S_N_FR)) > g(K_PAR)) need |= 8u;
-    if ((u64)g(S_NEXT_ORDER) + txn_len > g(K_MAP)) need |= 16u;
+    if (g(K_LEAF) - g(S_N_LEAVES) < 2ull * n_ops) need |= 1u;
+    if (g(K_CWO) == g(S_N_CWO) || g(K_TXN) == g(S_N_TXN)) need |= 2u;
+    if (g(K_DEL) - g(S_N_DEL) < n_dels) need |= 4u;
+    if (g(K_PAR) - g(S_N_PAR) < (remote ? n_parents : g(S_N_FR))) need |= 8u;
+    if (g(K_MAP) - g(S_NEXT_ORDER) < txn_len) need |= 16u;
     use_agent(agent);
-    if (g(T_AG_CNT) + 1 > g(T_AG_CAP)) need |= 32u;
+    if (g(T_AG_CAP) == g(T_AG_CNT)) need |= 32u;
     p(S_CAP_NEED, need);
     return need == 0;
   }
@@ -966,8 +1014,8 @@ struct Replayer {
         u32 o;
         i32 st = id_to_order(pr.w1 & 0xFFFFu, pr.w2, o);
         if (st != ST_OK) return st;
-        w.st(pp + j, o);
         if (j == 0) p0 = o;
+        else w.st(pp + j, o);  // pp[0] is written by insert_txn (only if the txn is kept)
       }
     }
     return insert_txn(remote, first, txn_len, np, p0);

@@ -36,17 +36,17 @@ struct WaveGPU {
   // compile-time lane numbers: v_readlane / v_writelane, no memory, no SGPR pressure.
   u32 x0 = 0, x1 = 0;
   __device__ __forceinline__ u32 xg(u32 f) const { return f < 64 ? rdlane(x0, f) : rdlane(x1, f - 64); }
-  __device__ __forceinline__ void xs(u32 f, u32 v) {
-    bool me = lane_id() == (f & 63u);
-    if (f < 64) x0 = me ? v : x0;
-    else x1 = me ? v : x1;
+  __device__ __forceinline__ void xs(u32 f, u32 v) {  // v_writelane (no lane mask to keep live)
+    u32 sv = uni(v);  // folds away for values the compiler already knows are uniform
+    if (f < 64) asm("v_writelane_b32 %0, %1, %2" : "+v"(x0) : "s"(sv), "n"(f));
+    else asm("v_writelane_b32 %0, %1, %2" : "+v"(x1) : "s"(sv), "n"(f - 64));
   }
   // DocState <-> slots [base, base + 20) of x0: one lane-parallel load / store
   __device__ __forceinline__ void x_load_state(const DocState* p, u32 base) {
     u32 l = lane_id();
     const u32* q = (const u32*)p;
     bool mine = l >= base && l < base + (u32)(sizeof(DocState) / 4);
-    u32 v = mine ? q[l - base] : 0u;
+    u32 v = q[mine ? l - base : 0u];  // clamped address: unconditional load, no exec branch
     x0 = mine ? v : x0;
   }
   __device__ __forceinline__ void x_store_state(DocState* p, u32 base) const {
@@ -121,7 +121,8 @@ struct WaveGPU {
     while (hi - lo > 64) {
       u32 step = (hi - lo + 63) / 64;
       u32 idx = lo + l * step;
-      bool ok = idx < hi && *(const u32*)&base[idx] <= needle;  // key is the first field
+      u32 key = *(const u32*)&base[idx < hi ? idx : hi - 1];  // key is the first field
+      bool ok = idx < hi && key <= needle;
       u64 m = ballot(ok);
       if (m == 0) return -1;
       u32 t = 63 - __builtin_clzll(m);
@@ -130,7 +131,8 @@ struct WaveGPU {
       hi = nh < hi ? nh : hi;
     }
     u32 idx = lo + l;
-    bool ok = idx < hi && *(const u32*)&base[idx] <= needle;
+    u32 key0 = *(const u32*)&base[idx < hi ? idx : hi - 1];
+    bool ok = idx < hi && key0 <= needle;
     u64 m = ballot(ok);
     if (m == 0) return -1;
     u32 k = lo + (63 - __builtin_clzll(m));
@@ -151,11 +153,10 @@ struct WaveGPU {
   // ---------------------------------------------------------------- leaf cache
   __device__ __forceinline__ u32 cache_load(const Span* p) {
     u32 l = lane_id();
-    if (l < (u32)L) {
-      uint4 v = *(const uint4*)(p + l);
-      eo = v.x; el = v.y; er = v.z; en = (i32)v.w;
-    } else { eo = el = er = 0; en = 0; }
-    return __popcll(ballot(l < (u32)L && en != 0));
+    bool in = l < (u32)L;
+    uint4 v = *(const uint4*)(p + (l & (u32)(L - 1)));  // lanes >= L re-read a valid entry
+    eo = in ? v.x : 0u; el = in ? v.y : 0u; er = in ? v.z : 0u; en = in ? (i32)v.w : 0;
+    return __popcll(ballot(en != 0));
   }
   __device__ __forceinline__ void cache_store(Span* p) const {
     u32 l = lane_id();
@@ -179,9 +180,9 @@ struct WaveGPU {
   // leaf.rs:41-57 find on a leaf that is NOT the cached one (peek: no cache change)
   __device__ __forceinline__ i32 peek_find_order(const Span* p, u32 order, u32& start) const {
     u32 l = lane_id();
-    u32 o = 0;
-    i32 n = 0;
-    if (l < (u32)L) { uint4 v = *(const uint4*)(p + l); o = v.x; n = (i32)v.w; }
+    uint4 v = *(const uint4*)(p + (l & (u32)(L - 1)));
+    u32 o = v.x;
+    i32 n = (i32)v.w;
     u32 sl = (u32)(n < 0 ? -n : n);
     u64 m = ballot(l < (u32)L && n != 0 && order >= o && order - o < sl);
     if (!m) return -1;
@@ -247,7 +248,8 @@ struct WaveGPU {
   u32 rx = 0, ry = 0, rz = 0, rw = 0;
   __device__ __forceinline__ void rec_block_load(const Rec* p, u32 n) {
     u32 l = lane_id();
-    if (l < n) { uint4 v = *(const uint4*)(p + l); rx = v.x; ry = v.y; rz = v.z; rw = v.w; }
+    uint4 v = *(const uint4*)(p + (l < n ? l : n - 1));  // n >= 1
+    rx = v.x; ry = v.y; rz = v.z; rw = v.w;
   }
   __device__ __forceinline__ Rec rec_get(u32 k) const {
     return Rec{rdlane(rx, k), rdlane(ry, k), rdlane(rz, k), rdlane(rw, k)};
@@ -292,7 +294,8 @@ struct WaveGPU {
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       if (r * 64 >= ng) break;
       u32 i = r * 64 + l;
-      u64 m = ballot(i < ng && rblk()[i] == blk);
+      u32 b = rblk()[i];  // i < MAX_GROUPS: always inside this wave's LDS slice
+      u64 m = ballot(i < ng && b == blk);
       if (m) return r * 64 + __builtin_ctzll(m);
     }
     return INVALID;
@@ -314,10 +317,10 @@ struct WaveGPU {
     for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
       u32 i = r * 64 + l;
       u32 j = i - 1;
-      bool mv = i > g && i <= ng;
-      b[r] = mv ? rblk()[j] : 0u;
-      c[r] = mv ? rcnt()[j] : 0u;
-      v[r] = mv ? rvis()[j] : 0u;
+      u32 jj = j & (MAX_GROUPS - 1);
+      b[r] = rblk()[jj];
+      c[r] = rcnt()[jj];
+      v[r] = rvis()[jj];
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -337,7 +340,8 @@ struct WaveGPU {
       if (r * 64 >= ng) break;
       u32 i = r * 64 + l;
       bool valid = i < ng;
-      u32 x = valid ? rvis()[i] : 0u;
+      u32 xv = rvis()[i];
+      u32 x = valid ? xv : 0u;
       u32 incl = wave_incl_scan(x) + carry;
       u32 nvalid = ng - r * 64 < 64 ? ng - r * 64 : 64;
       u32 k = __popcll(ballot(valid && incl <= pos));
@@ -356,8 +360,8 @@ struct WaveGPU {
   // rows are loaded together so the descent costs one HBM round trip)
   __device__ __forceinline__ bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
     u32 l = lane_id();
-    u32 x = 0, lf = 0;
-    if (l < cnt) { x = dv[l]; lf = dl[l]; }
+    u32 xv = dv[l], lf = dl[l];  // block rows are 64 slots wide: always in bounds
+    u32 x = l < cnt ? xv : 0u;
     u32 incl = wave_incl_scan(x);
     u32 k = __popcll(ballot(l < cnt && incl <= rem));
     if (k >= cnt) return false;
@@ -368,8 +372,8 @@ struct WaveGPU {
   }
   __device__ __forceinline__ void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
     u32 l = lane_id();
-    u32 ol = l < cnt ? *(u32*)(dl + l) : 0u;
-    u32 ov = l < cnt ? *(u32*)(dv + l) : 0u;
+    u32 ol = *(u32*)(dl + l);
+    u32 ov = *(u32*)(dv + l);
     u32 sl = shfl(ol, l - 1), sv = shfl(ov, l - 1);
     u32 nlf = l < i ? ol : (l == i ? leaf : sl);
     u32 nvs = l < i ? ov : (l == i ? vis : sv);
