@@ -19,6 +19,7 @@ struct WaveCPU {
   // context registers (plain array: slot f)
   u32 x[128] = {};
   u32 xg(u32 f) const { return x[f]; }
+  template <class T> static T* gptr(u64 v) { return (T*)v; }
   void xs(u32 f, u32 v) { x[f] = v; }
   void x_load_state(const DocState* p, u32 base) { std::memcpy(x + base, p, sizeof(DocState)); }
   void x_store_state(DocState* p, u32 base) const { std::memcpy(p, x + base, sizeof(DocState)); }

@@ -79,7 +79,8 @@ struct Replayer {
   CRDT_HD u32 g(u32 f) const { return w.xg(f); }
   CRDT_HD void p(u32 f, u32 v) { w.xs(f, v); }
   CRDT_HD void inc(u32 f, u32 d = 1) { w.xs(f, w.xg(f) + d); }
-  template <class T> CRDT_HD T* ptr(u32 f) const { return (T*)(((u64)w.xg(f + 1) << 32) | w.xg(f)); }
+  // (W::gptr tells the compiler the address is global memory: global_load/store, not flat)
+  template <class T> CRDT_HD T* ptr(u32 f) const { return w.template gptr<T>(((u64)w.xg(f + 1) << 32) | w.xg(f)); }
   CRDT_HD void pset(u32 f, const void* q) {
     u64 v = (u64)q;
     w.xs(f, (u32)v);

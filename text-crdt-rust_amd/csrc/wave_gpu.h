@@ -41,6 +41,13 @@ struct WaveGPU {
     if (f < 64) asm("v_writelane_b32 %0, %1, %2" : "+v"(x0) : "s"(sv), "n"(f));
     else asm("v_writelane_b32 %0, %1, %2" : "+v"(x1) : "s"(sv), "n"(f - 64));
   }
+  // A pointer rebuilt from context lanes is a plain integer to the compiler; casting through
+  // address space 1 lets it emit global_load/store (vmcnt only) instead of flat ops, which
+  // also count in lgkmcnt and so would make every LDS wait drain all pending stores.
+  template <class T> __device__ __forceinline__ static T* gptr(u64 v) {
+    typedef __attribute__((address_space(1))) T GT;
+    return (T*)(GT*)v;
+  }
   // DocState <-> slots [base, base + 20) of x0: one lane-parallel load / store
   __device__ __forceinline__ void x_load_state(const DocState* p, u32 base) {
     u32 l = lane_id();
