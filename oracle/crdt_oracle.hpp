@@ -590,7 +590,11 @@ inline void increment_delete_range(std::vector<DDRun>& v, u32 base, u32 len) {
   size_t idx = s >= 0 ? (size_t)s : (size_t)(-s - 1);
   auto dd_can_append = [](const DDRun& a, const DDRun& b) { return b.key == a.key + a.len && b.excess == a.excess; };
   while (true) {
-    if (idx == v.size() || v[idx].key > next.key) {
+    // Quirk Q9: the gap test compares against `base`, not `next.key` (double_delete.rs:52).
+    // When a later iteration reaches an adjacent run (v[idx].key == next.key > base) release
+    // builds take the gap branch and insert a zero-length entry (truncate(0); the debug
+    // assertion at rle/mod.rs:34 is compiled out).  The digest sees those entries.
+    if (idx == v.size() || v[idx].key > base) {
       DDRun here = next;
       bool done_here;
       if (idx < v.size() && next.key + next.len > v[idx].key) {

@@ -115,6 +115,29 @@ struct WaveCPU {
   Rec rb[64];
   void rec_block_load(const Rec* p, u32 n) { for (u32 i = 0; i < n; i++) rb[i] = p[i]; }
   Rec rec_get(u32 k) const { return rb[k]; }
+  u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 ow1, u32 ow3, u32& total) const {
+    u32 per = remote ? 3u : 2u;
+    u32 n = 1;
+    total = rb[b0].w3;
+    for (u32 j = b0 + per; j + per <= nv; j += per) {
+      const Rec &h = rb[j], &o = rb[j + 1], &ph = rb[j - per], &po = rb[j - per + 1];
+      bool ok;
+      if (remote) {
+        const Rec& pr = rb[j + 2];
+        ok = h.w0 == ((REC_RTXN << 28) | 1u) && h.w1 == (agent | (1u << 16)) && h.w2 == ph.w2 + ph.w3 &&
+             h.w3 - 1u < 0xFFFFu && (o.w0 >> 28) == REC_RINS && (o.w0 & 0x0FFFFFFFu) == h.w3 && o.w1 == ow1 &&
+             o.w3 == ow3 && o.w2 == h.w2 - 1u && pr.w0 == (REC_RPARENT << 28) && pr.w1 == agent && pr.w2 == h.w2 - 1u;
+      } else {
+        ok = h.w0 == ((REC_LTXN << 28) | 1u) && h.w1 == agent && h.w2 == 0u && h.w3 - 1u < 0xFFFFu &&
+             o.w0 == (REC_LOP << 28) && o.w2 == 0u && o.w3 == h.w3 && o.w1 == po.w1 + po.w3;
+      }
+      (void)ph;
+      if (!ok) break;
+      n++;
+      total += h.w3;
+    }
+    return n;
+  }
 
   // directory root
   void root_init(u32 blk, u32 cnt, u32 vis) {

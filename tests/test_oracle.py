@@ -58,6 +58,23 @@ def test_inc_delete_range():
     assert d.get() == [(4, 1, 1), (5, 1, 3), (6, 1, 2), (7, 1, 3), (8, 2, 1)]
 
 
+def test_inc_delete_range_adjacent_run_quirk():
+    # Quirk Q9 (double_delete.rs:52 tests `self.0[idx].0 > base`): after incrementing (5,3) the
+    # loop reaches the adjacent run at 8 (key 8 == next key > base 5) and takes the gap branch
+    # with a zero-length remainder, which release builds insert as an entry of length 0
+    # (rle/mod.rs:34's debug_assert is compiled out).  Release semantics, hand-derived.
+    d = DoubleDeletes()
+    d.increment(5, 3)
+    d.increment(5, 3)
+    d.increment(8, 2)
+    assert d.get() == [(5, 3, 2), (8, 2, 1)]
+    d.increment(5, 5)
+    assert d.get() == [(5, 3, 3), (8, 0, 1), (8, 2, 2)]
+    # zero-length entries are counted as entries of the run they precede and multiply
+    d.increment(3, 6)
+    assert d.get() == [(3, 2, 1), (5, 3, 4), (8, 0, 1), (8, 0, 2), (8, 0, 1), (8, 1, 3), (9, 1, 2)]
+
+
 # --- benches/yjs.rs:39,46: final doc.len() == endContent.len() --------------------------------
 @pytest.mark.parametrize("name", TRACE_NAMES)
 @pytest.mark.parametrize("caps", [(32, 16), (4, 8)])

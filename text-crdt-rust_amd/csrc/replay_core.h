@@ -681,7 +681,7 @@ struct Replayer {
       while (idx < g(S_N_DD) && w.ld_dd(b + idx).key <= base) idx++;
     }
     while (true) {
-      if (idx == g(S_N_DD) || w.ld_dd(b + idx).key > next.key) {
+      if (idx == g(S_N_DD) || w.ld_dd(b + idx).key > base) {  // quirk Q9 (double_delete.rs:52)
         DDRun here = next;
         bool done_here;
         if (idx < g(S_N_DD) && next.key + next.len > w.ld_dd(b + idx).key) {
@@ -1022,6 +1022,165 @@ struct Replayer {
     return insert_txn(remote, first, txn_len, np, p0);
   }
 
+  // ------------------------------------------------------------------ fast paths
+  // Real edit traces are dominated by two single-op txn shapes: typing (an insert right after
+  // the agent's previous item) and a delete inside one visible entry.  For those, apply_txn's
+  // effects reduce to a few context updates, so they are recognised up front -- every condition
+  // apply_txn would evaluate is checked against the same state before anything changes -- and
+  // applied directly; everything else takes the general interpreter.  A typing run is validated
+  // for the rest of the 64-record prefetch block at once, lane-parallel (W::typing_scan), and
+  // applied as one append.
+  //
+  // Txn level (doc.rs:155-165 assign_order_to_client, doc.rs:350-374 insert_txn): the txn
+  // continues its agent's last item_orders run and the last client_with_order run, its single
+  // parent is the previous order, the frontier is that one order, so the txn coalesces into the
+  // last TxnSpan (TxnSpan::can_append, txn.rs:44-48: shadow unchanged, parents not kept).
+  CRDT_HD u32 fast_txn_ok(u32 agent, u32 seq, u32 first) const {
+    u32 ll = g(T_AGL_LEN), cl = g(T_CWO_LEN);
+    return (agent == g(T_AG_ID)) & (g(T_AG_CNT) != 0u) & (seq == g(T_AGL_KEY) + ll) &
+           (g(T_AGL_ORDER) + ll == first) & (g(S_N_CWO) != 0u) & (g(T_CWO_AGENT) == agent) &
+           (g(T_CWO_SEQ) + cl == seq) & (g(T_CWO_KEY) + cl == first) & (g(S_N_FR) == 1u) &
+           (g(T_FR0) == first - 1u) & (g(S_N_TXN) != 0u) & (g(T_TX_ORDER) + g(T_TX_LEN) == first);
+  }
+  CRDT_HD void fast_txn_commit(u32 first, u32 len) {
+    p(S_NEXT_ORDER, first + len);
+    inc(T_CWO_LEN, len);
+    inc(T_AGL_LEN, len);
+    p(T_FR0, first + len - 1u);
+    inc(T_TX_LEN, len);
+    p(S_CAP_NEED, 0u);
+  }
+  // the first order after entry idx of the cached leaf (get_item at the entry's end, cursor.rs:233-239)
+  CRDT_HD u32 next_item_after(u32 idx, u32& order) {
+    if (idx + 1u < g(C_N)) { order = w.cget_order(idx + 1u); return 1u; }
+    u32 fo;
+    u32 has = cached_succ(fo) != INVALID;
+    order = fo;
+    return has;
+  }
+  // Typing: origin_left = the previous txn's last item = the last item of entry idx,
+  // origin_right = the item after that entry (or none).  integrate stops at once (doc.rs:184-190)
+  // and insert_internal appends to the entry (mutations.rs:57-80, YjsSpan::can_append); every
+  // later txn of the run is the same case.  Returns records consumed (0: not applicable).
+  CRDT_HD u32 fast_typing(u32 b0, u32 nv, u32 remote, u32 idx, u32 orr, u32 agent, const Rec& o, u32 first) {
+    Span e = w.cget(idx);
+    if (!((e.len > 0) & (e.order + (u32)e.len == first) & (e.orr == orr))) return 0;
+    u32 total;
+    u32 nt = w.typing_scan(b0, nv, remote, agent, o.w1, o.w3, total);
+    if (g(K_MAP) - first < total) return 0;     // capacity: the general path stops exactly
+    w.fill(lof() + first, total, g(C_LEAF));   // notify (doc.rs:143-153)
+    e.len += (i32)total;
+    set(idx, e);
+    inc(S_N_ITEMS, total);
+    fast_txn_commit(first, total);
+    return nt * (remote ? 3u : 2u);
+  }
+  // Delete `l` items at offset `off` of visible entry idx of the cached leaf: mutate_entry
+  // (mutations.rs:227-277) and insert_internal's prepend / shift (mutations.rs:84-146) without a
+  // leaf split.  Returns 0, having changed nothing, when a split or a table growth is needed.
+  CRDT_HD u32 fast_delete(u32 idx, u32 off, u32 l, u32 first) {
+    if ((g(K_MAP) - first < l) | (g(K_DEL) == g(S_N_DEL))) return 0;
+    Span e = w.cget(idx);
+    u32 n = g(C_N);
+    u32 target = e.order + off;
+    u32 ha = off > 0u, hc = off + l < (u32)e.len;
+    Span pa{e.order, e.ol, e.orr, (i32)off};
+    Span dd{target, ha ? target - 1u : e.ol, e.orr, -(i32)l};
+    Span pc{target + l, target + l - 1u, e.orr, e.len - (i32)(off + l)};
+    Span x0 = ha ? dd : pc;  // pieces after the cursor entry: [x0, pc][:m]
+    u32 m = ha + hc;
+    u32 pre = 0;
+    Span nx{0, 0, 0, 0};
+    if (m != 0u && idx + 1u < n) {
+      nx = w.cget(idx + 1u);
+      Span last = m == 2u ? pc : x0;
+      if (can_append(last, nx)) {
+        nx.order = last.order;  // YjsSpan::prepend keeps origin_left (span.rs:61-64)
+        nx.len += last.len;
+        pre = 1;
+        m -= 1u;
+      }
+    }
+    if (n + m > (u32)L) return 0;
+    set(idx, ha ? pa : dd);
+    if (pre) set(idx + 1u, nx);
+    if (m) {
+      w.cache_shift_right(idx + 1u, n, m);
+      p(C_N, n + m);
+      set(idx + 1u, x0);
+      if (m == 2u) set(idx + 2u, pc);
+      inc(S_N_ENTRIES, m);
+    }
+    append_delete(first, target, l);    // doc.rs:305-308 / 420-423
+    w.fill(lof() + first, l, INVALID);  // delete orders name no item
+    fast_txn_commit(first, l);
+    return 1;
+  }
+  // Returns the records consumed by a fast-path txn at `pos`, or 0 (use apply_txn).
+  CRDT_HD u32 fast_txn(u32 pos, u32 kind) {
+    u32 remote = kind == REC_RTXN;
+    u32 per = remote ? 3u : 2u;
+    u32 rn = rec_n();
+    if ((rn - pos < per) | (g(C_LEAF) == INVALID)) return 0;
+    u32 b0 = pos - g(T_RB_BASE);
+    if (b0 + per > 64u) {  // re-base the prefetch block: the txn and what follows it
+      u32 nn = rn - pos;
+      p(T_RB_BASE, pos);
+      w.rec_block_load(recs() + pos, nn < 64u ? nn : 64u);
+      b0 = 0;
+    }
+    u32 nv = rn - g(T_RB_BASE);
+    nv = nv < 64u ? nv : 64u;
+    Rec h = w.rec_get(b0), o = w.rec_get(b0 + 1u);
+    u32 first = g(S_NEXT_ORDER);
+    u32 idx, off, l;
+    if (remote) {
+      Rec pr = w.rec_get(b0 + 2u);
+      u32 agent = h.w1 & 0xFFFFu, seq = h.w2;
+      l = o.w0 & 0x0FFFFFFFu;
+      u32 ok = (h.w0 == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
+               (pr.w0 == (REC_RPARENT << 28)) & (pr.w1 == agent) & (pr.w2 == seq - 1u);
+      if (!ok || !fast_txn_ok(agent, seq, first)) return 0;
+      u32 k = rec_kind(o);
+      if (k == REC_RINS) {
+        if (!(((o.w1 & 0xFFFFu) == agent) & (o.w2 == seq - 1u))) return 0;  // origin_left = first - 1
+        u32 orr;
+        if (id_to_order(o.w1 >> 16, o.w3, orr) != ST_OK) return 0;
+        i32 x = w.cfind_order(g(C_N), first - 1u);
+        if (x < 0) return 0;
+        u32 nxo, has = next_item_after((u32)x, nxo);
+        if (has && nxo != orr) return 0;  // integrate would scan (doc.rs:183-221)
+        return fast_typing(b0, nv, 1u, (u32)x, orr, agent, o, first);
+      }
+      u32 target;
+      if (k != REC_RDEL || id_to_order(o.w1 & 0xFFFFu, o.w2, target) != ST_OK || target == ROOT_ORDER) return 0;
+      i32 x = w.cfind_order(g(C_N), target);
+      if (x < 0) return 0;
+      idx = (u32)x;
+      i32 el = w.cget_len(idx);
+      off = target - w.cget_order(idx);
+      if ((el <= 0) | (off + l > (u32)el)) return 0;  // already deleted / spans entries
+    } else {
+      u32 agent = h.w1, lp = o.w1, del = o.w2, ins = o.w3;
+      l = del + ins;
+      u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l) &
+               ((del == 0u) != (ins == 0u)) & (l - 1u < 0xFFFFu) & (g(C_VS_OK) != 0u) & ((ins == 0u) | (lp != 0u));
+      if (!ok || !fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first)) return 0;
+      u32 at = ins ? lp - 1u : lp;  // insert: origin_left is the item at pos - 1 (doc.rs:446-447)
+      u32 vs = g(C_VSTART);
+      if ((at < vs) | (at - vs >= g(C_NOW))) return 0;  // outside the cached leaf's visible range
+      if (!w.cfind_content(g(C_N), at - vs, idx, off)) return 0;
+      i32 el = w.cget_len(idx);
+      if (ins) {
+        if (off + 1u != (u32)el) return 0;  // origin_left ends its entry
+        u32 nxo, has = next_item_after(idx, nxo);
+        return fast_typing(b0, nv, 0u, idx, has ? nxo : ROOT_ORDER, agent, o, first);
+      }
+      if (off + l > (u32)el) return 0;
+    }
+    return fast_delete(idx, off, l, first) ? per : 0u;
+  }
+
   // Replay this document's record stream from its rec_pos.
   CRDT_HD void run() {
     u32 pos = g(S_REC_POS);
@@ -1032,6 +1191,8 @@ struct Replayer {
       i32 st;
       u32 consumed;
       if (kind == REC_LTXN || kind == REC_RTXN) {
+        u32 fast = fast_txn(pos, kind);
+        if (fast) { pos += fast; continue; }
         bool remote = kind == REC_RTXN;
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
         consumed = 1 + nops + (remote ? (h.w1 >> 16) : 0u);

@@ -261,6 +261,38 @@ struct WaveGPU {
   __device__ __forceinline__ Rec rec_get(u32 k) const {
     return Rec{rdlane(rx, k), rdlane(ry, k), rdlane(rz, k), rdlane(rw, k)};
   }
+  // Typing-run scan (replay_core.h fast_typing): lane k checks record k of the prefetch block
+  // against "txn continues the typing txn before it" -- remote: RTXN{1 op, 1 parent}, RINS with
+  // origin_left = (agent, seq-1) and the same origin_right, RPARENT (agent, seq-1), seq = previous
+  // seq + previous length; local: LTXN{1 op}, LOP insert at the previous pos + previous length.
+  // The txn at b0 was checked by the caller.  Returns the run length in txns (>= 1) and the
+  // total inserted length.  nv = valid records in the block.
+  __device__ __forceinline__ u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 ow1, u32 ow3, u32& total) const {
+    u32 l = lane_id();
+    u32 rel = l - b0;  // wraps below b0: those lanes are masked
+    u32 per = remote ? 3u : 2u;
+    u32 t = remote ? (rel * 43u) >> 7 : rel >> 1;  // rel / 3 exactly for rel < 64
+    u32 r = rel - t * per;
+    bool ok;
+    if (remote) {
+      u32 src = r == 0u ? l - 3u : (r == 1u ? l - 1u : l - 2u);  // previous header / own header
+      u32 hs = shfl(rz, src), hl = shfl(rw, src);
+      bool okh = rx == ((REC_RTXN << 28) | 1u) && ry == (agent | (1u << 16)) && rz == hs + hl && rw - 1u < 0xFFFFu;
+      bool oko = (rx >> 28) == REC_RINS && (rx & 0x0FFFFFFFu) == hl && ry == ow1 && rw == ow3 && rz == hs - 1u;
+      bool okp = rx == (REC_RPARENT << 28) && ry == agent && rz == hs - 1u;
+      ok = r == 0u ? okh : (r == 1u ? oko : okp);
+    } else {
+      u32 hl = shfl(rw, l - 1u), ps = shfl(ry, l - 2u), pl = shfl(rw, l - 2u);
+      bool okh = rx == ((REC_LTXN << 28) | 1u) && ry == agent && rz == 0u && rw - 1u < 0xFFFFu;
+      bool oko = rx == (REC_LOP << 28) && rz == 0u && rw == hl && ry == ps + pl;
+      ok = r == 0u ? okh : oko;
+    }
+    u64 stop = ballot(l >= b0 + per && (!ok || l >= nv));
+    u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
+    u32 n = remote ? ((f - b0) * 43u) >> 7 : (f - b0) >> 1;
+    total = wave_sum(l >= b0 && r == 0u && t < n ? rw : 0u);
+    return n;
+  }
 
   // ---------------------------------------------------------------- directory root (VGPRs)
   __device__ __forceinline__ u32* rblk() const { return rt; }
