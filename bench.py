@@ -71,6 +71,59 @@ def cpu_baseline(wire: bytes, n_docs: int, threads: int):
     return secs
 
 
+def cpu_baseline_sampled(wire: bytes, threads: int, target_s: float, max_docs: int = 16384):
+    """Bounded sample: one calibration pass (one document per thread), then as many documents as
+    fill about `target_s` seconds.  Returns (docs, seconds)."""
+    t_cal = cpu_baseline(wire, threads, threads)
+    per_doc = max(t_cal / threads, 1e-4)
+    n = int(min(max_docs, max(threads, target_s / per_doc)))
+    return n, cpu_baseline(wire, n, threads)
+
+
+def shard(rank: int, world: int, docs_per_rank: int):
+    """Weak scaling: rank r owns documents [r*n, (r+1)*n) of the global corpus (no
+    per-op communication between ranks)."""
+    assert 0 <= rank < world
+    return rank * docs_per_rank, docs_per_rank
+
+
+def reduce_over_ranks(elapsed: float, digests: np.ndarray, dist, device):
+    """The only collectives: max of the per-rank elapsed time, and one all-gather of the per-
+    document u64 digests (RCCL on the GPU path, gloo in the CPU rehearsal test)."""
+    import torch
+    if dist is None:
+        return elapsed, digests
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    g = torch.from_numpy(np.ascontiguousarray(digests).view(np.int64)).to(device)
+    outs = [torch.empty_like(g) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, g)
+    return float(t.item()), torch.cat(outs).cpu().numpy().view(np.uint64)
+
+
+def golden_digest(trace: str):
+    """Committed fixture (tests/golden/oracle_golden.json): the oracle's digest of the trace's
+    remote replay with the release layout.  Every document of the bench must reproduce it."""
+    import json
+    p = os.path.join(ROOT, "tests", "golden", "oracle_golden.json")
+    try:
+        return int(json.load(open(p))[f"{trace}/L32"]["remote_digest"], 16)
+    except (OSError, KeyError):
+        return None
+
+
+def measured_traffic(n_docs: int):
+    """HBM bytes per k_replay launch from the committed PMC pass (profiles/traffic_k_replay.json:
+    FETCH_SIZE x 2 + WRITE_SIZE per the MI355X guide's gfx950 correction), scaled per document."""
+    import json
+    p = os.path.join(ROOT, "profiles", "traffic_k_replay.json")
+    try:
+        t = json.load(open(p))
+        return t["hbm_bytes_per_launch"] / t["docs"] * n_docs
+    except (OSError, KeyError, ZeroDivisionError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,7 +131,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--docs", type=int, default=4096, help="documents per GPU")
     ap.add_argument("--trace", default="automerge-paper")
-    ap.add_argument("--cpu-docs", type=int, default=64, help="documents in the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
     args = ap.parse_args()
@@ -98,8 +151,7 @@ def main():
 
     wire = load_remote_wire(args.trace)
     n_ops_doc, n_recs_doc, n_txn_doc = wire_ops(wire)
-    n = args.docs
-    doc0 = rank * n
+    doc0, n = shard(rank, world, args.docs)
     names = [doc_name(doc0 + i) for i in range(n)]
     # the wire's name table: index 0 is "jeremy" (the trace author); replace it per document
     eng = crdt_amd.Engine(n, 32, device=local_rank if world > 1 else 0)
@@ -173,19 +225,9 @@ def main():
     st = eng.status()
     ok = bool((st == 0).all())
     dg = eng.digests()
-    t_max = elapsed
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
-        # the one collective of the design: all-gather of per-document state digests over RCCL
-        g = torch.from_numpy(dg.view(np.int64)).to(dev)
-        outs = [torch.empty_like(g) for _ in range(world)]
-        dist.all_gather(outs, g)
-        all_dg = torch.cat(outs).cpu().numpy().view(np.uint64)
-        ok = ok and bool((all_dg == all_dg[0]).all())
-    else:
-        ok = ok and bool((dg == dg[0]).all())
+    t_max, all_dg = reduce_over_ranks(elapsed, dg, dist, dev)
+    gold = golden_digest(args.trace)
+    ok = ok and bool((all_dg == all_dg[0]).all()) and (gold is None or int(all_dg[0]) == gold)
     total_ops = n_ops_doc * n * world * args.steps
     value = total_ops / t_max
     ms_step = t_max / args.steps * 1e3
@@ -202,8 +244,7 @@ def main():
         cpu = None
         if not args.no_cpu:
             threads = min(16, os.cpu_count() or 1)
-            cd = args.cpu_docs
-            secs = cpu_baseline(wire, cd, threads)
+            cd, secs = cpu_baseline_sampled(wire, threads, args.cpu_seconds)
             cpu = {"value": n_ops_doc * cd / secs, "unit": "ops/s", "cores": threads, "kind": "port",
                    "sample": f"{cd} docs x {args.trace} remote replay ({n_ops_doc} ops each), oracle C++ "
                              f"restatement of the reference B-tree path (leaf 32/node 16), {threads} threads, "
@@ -225,11 +266,12 @@ def main():
                                    f"replay+publish+{q} pos->loc & loc->pos queries/doc",
                        "docs_per_gpu": n, "ops_per_doc": n_ops_doc, "parallelism": f"doc-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": (achieved / 8000.0) if achieved else None, "traffic": None,
+                         "frac": (achieved / 8000.0) if achieved else None, "traffic": measured_traffic(n),
                          "kernel": "k_replay<32>", "kernel_ms": rms,
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
             "parity_ok": ok,
+            "parity": "every document's digest == committed oracle golden digest (tests/golden)",
             "stage_s": stage_s,
         }
         print(json.dumps(out))

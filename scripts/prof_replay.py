@@ -1,4 +1,6 @@
-"""Profiling driver: stage `docs` copies of a trace's remote form and run ONE replay + publish."""
+"""Profiling driver: stage `docs` copies of a trace's remote form, replay (with capacity growth),
+then with --clean reset and replay once more as ONE k_replay launch (what bench.py times), and
+publish.  The last k_replay dispatch of the process is the clean one."""
 import argparse
 import os
 import sys
@@ -13,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--docs", type=int, default=64)
 ap.add_argument("--trace", default="automerge-paper")
 ap.add_argument("--local", action="store_true")
+ap.add_argument("--clean", action="store_true", help="reset and replay once more (single launch)")
 a = ap.parse_args()
 e = crdt_amd.Engine(a.docs, 32)
 if a.local:
@@ -24,6 +27,11 @@ else:
     e.stage_remote_replicated(w, 0, ["u%05d" % i for i in range(a.docs)])
 t0 = time.time()
 st = e.run()
+if a.clean:
+    e.reset_async()
+    e.run_async()
+    e.sync()
+    st = e.status()
 e.publish_async()
 e.sync()
 print("status ok:", bool((st == 0).all()), "replay_ms", e.timings()[0], "wall", time.time() - t0)
