@@ -74,8 +74,8 @@ def cpu_baseline(wire: bytes, n_docs: int, threads: int):
 def cpu_baseline_sampled(wire: bytes, threads: int, target_s: float, max_docs: int = 16384):
     """Bounded sample: one calibration pass (one document per thread), then as many documents as
     fill about `target_s` seconds.  Returns (docs, seconds)."""
-    t_cal = cpu_baseline(wire, threads, threads)
-    per_doc = max(t_cal / threads, 1e-4)
+    t_cal = cpu_baseline(wire, 4 * threads, threads)
+    per_doc = max(t_cal / (4 * threads), 1e-4)
     n = int(min(max_docs, max(threads, target_s / per_doc)))
     return n, cpu_baseline(wire, n, threads)
 
@@ -131,7 +131,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--docs", type=int, default=4096, help="documents per GPU")
     ap.add_argument("--trace", default="automerge-paper")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target length of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
     args = ap.parse_args()
