@@ -102,6 +102,13 @@ int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs
  * batch's name table is replaced per document by names[d] (randomised client ids). */
 int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t wire_len,
                                  uint32_t rename_idx, const char* const* names);
+/* On-device edit generator (BASELINE config 4): each document docs[i] gets n_ops local txns by
+ * `agent`, one LocalOp each, drawn on the GPU inside the replay wave with the semantics of the
+ * reference's make_random_change (doc.rs:544-569; insert 1 char w.p. 0.55 below 100 chars else
+ * 0.45, delete 1..10 chars).  Per-document seed = low 32 bits of splitmix64(seed ^ doc).  Only
+ * one GEN record per document is staged, so 10^6 documents need no host-side op stream. */
+int crdt_stage_random(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const char* agent, uint32_t n_ops,
+                      uint64_t seed);
 /* Reset every document to ListCRDT::new() state, keeping interned agents and staged records. */
 int crdt_reset_async(crdt_engine* e);
 /* Replay the staged records of every document (+ capacity growth/resume as needed). */

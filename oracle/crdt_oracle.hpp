@@ -950,6 +950,28 @@ struct Doc {
 };
 
 // ---------------------------------------------------------------------------------------------
+// Random edit generator (BASELINE config 4): the semantics of make_random_change (doc.rs:544-569)
+// drawn from a counter-based hash of (seed, op#) (the reference's SmallRng stream is Rust-only).
+// Must match gen_op in text-crdt-rust_amd/csrc/crdt_types.h draw for draw.
+// ---------------------------------------------------------------------------------------------
+inline u64 gen_mix64(u64 z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline LocalOp random_change(u32 seed, u32 i, u32 len) {
+  u64 r = gen_mix64(((u64)seed << 32) | i);
+  u32 hi = (u32)(r >> 32), lo = (u32)r;
+  u32 thr = len < 100u ? 0x8CCCCCCDu : 0x73333333u;  // P(insert) = 0.55 below 100 chars, else 0.45
+  if (len == 0u || hi < thr) return LocalOp{(u32)(((u64)lo * (len + 1u)) >> 32), 0u, 1u};  // pos U[0, len]
+  u32 pos = (u32)(((u64)lo * len) >> 32);                                              // U[0, len-1]
+  u32 mx = std::min<u32>(10u, len - pos);
+  u32 r2 = (u32)gen_mix64(r);
+  return LocalOp{pos, 1u + (u32)(((u64)r2 * mx) >> 32), 0u};                           // U[1, mx]
+}
+
+// ---------------------------------------------------------------------------------------------
 // Digest (definition shared with the GPU digest kernel; see DESIGN.md "Digest")
 // ---------------------------------------------------------------------------------------------
 inline u64 mix64(u64 z) {  // splitmix64 finaliser

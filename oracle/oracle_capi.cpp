@@ -125,6 +125,17 @@ int orc_apply_local_trace(void* h, uint16_t agent, uint32_t ntxn, const uint32_t
   return OK;
 }
 
+// n_ops generated local edits by `agent` (config 4), one LocalOp per txn.
+int orc_apply_random(void* h, uint16_t agent, uint32_t n_ops, uint32_t seed) {
+  Doc* d = (Doc*)h;
+  for (uint32_t i = 0; i < n_ops; i++) {
+    LocalOp op = random_change(seed, i, d->len());
+    int st = d->apply_local_txn(agent, &op, 1);
+    if (st != OK) return st;
+  }
+  return OK;
+}
+
 int orc_apply_remote_wire(void* h, const uint8_t* buf, size_t len) {
   Doc* d = (Doc*)h;
   wire::Batch b;

@@ -179,6 +179,15 @@ int emu_run_local(void* h, uint16_t agent, uint32_t ntxn, const uint32_t* counts
   return d->run();
 }
 
+int emu_run_random(void* h, uint16_t agent, uint32_t n_ops, uint32_t seed, uint32_t leaf_div) {
+  EmuDoc* d = (EmuDoc*)h;
+  StreamNeeds nd;
+  d->recs.clear();
+  encode_gen(d->recs, nd, agent, n_ops, seed);
+  d->prepare(nd, true, leaf_div);
+  return d->run();
+}
+
 int emu_run_wire(void* h, const uint8_t* wire, size_t len, uint32_t leaf_div) {
   EmuDoc* d = (EmuDoc*)h;
   WireView wv;

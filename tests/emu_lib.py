@@ -33,6 +33,7 @@ def lib():
         L.emu_agent.argtypes = [vp, C.c_char_p]
         L.emu_run_local.argtypes = [vp, u16, u32, P(u32), P(u32), u32]
         L.emu_run_wire.argtypes = [vp, C.c_char_p, C.c_size_t, u32]
+        L.emu_run_random.argtypes = [vp, u16, u32, u32, u32]
         L.emu_sizes.argtypes = [vp, P(C.c_uint64)]
         L.emu_export.argtypes = [vp] + [P(u32)] * 8
         L.emu_check.argtypes = [vp, C.c_char_p, C.c_int]
@@ -63,6 +64,9 @@ class EmuDoc:
 
     def run_wire(self, wire: bytes, leaf_div: int = 48) -> int:
         return self.L.emu_run_wire(self.h, wire, len(wire), leaf_div)
+
+    def run_random(self, agent: int, n_ops: int, seed32: int, leaf_div: int = 48) -> int:
+        return self.L.emu_run_random(self.h, agent, n_ops, seed32 & 0xFFFFFFFF, leaf_div)
 
     def check(self) -> str:
         buf = C.create_string_buffer(512)

@@ -44,6 +44,7 @@ def lib():
     L.orc_agent.argtypes = [vp, C.c_char_p]
     L.orc_apply_local.argtypes = [vp, u16, u32, P(u32)]
     L.orc_apply_local_trace.argtypes = [vp, u16, u32, P(u32), P(u32)]
+    L.orc_apply_random.argtypes = [vp, u16, u32, u32]
     L.orc_apply_remote_wire.argtypes = [vp, C.c_char_p, C.c_size_t]
     L.orc_local_trace_to_wire.argtypes = [vp, u16, u32, P(u32), P(u32), C.c_void_p, i64]
     L.orc_local_trace_to_wire.restype = i64
@@ -103,6 +104,10 @@ class OracleDoc:
 
     def apply_remote_wire(self, wire: bytes) -> int:
         return self.L.orc_apply_remote_wire(self.h, wire, len(wire))
+
+    def apply_random(self, agent: int, n_ops: int, seed32: int) -> int:
+        """config 4 generator (crdt_oracle.hpp random_change), n_ops local txns."""
+        return self.L.orc_apply_random(self.h, agent, n_ops, seed32 & 0xFFFFFFFF)
 
     def trace_to_wire(self, agent: int, counts, patches) -> bytes:
         c = np.ascontiguousarray(counts, dtype=np.uint32)

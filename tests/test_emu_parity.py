@@ -50,3 +50,17 @@ def test_concurrent(seed):
         if so == 0:
             assert e.check() == ""
             assert diff_states(o.export(), e.export()) == []
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_generated_config4(seed):
+    # BASELINE config 4 generator (make_random_change, doc.rs:544-569) expanded inside the replay
+    # loop from one GEN record; the oracle draws the same ops (crdt_oracle.hpp random_change).
+    n_ops = 3000 + 500 * seed
+    for L in (32, 4):
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        assert o.apply_random(o.agent("gen"), n_ops, 0x9E3779B9 * (seed + 1)) == 0
+        e = EmuDoc(L)
+        assert e.run_random(e.agent("gen"), n_ops, 0x9E3779B9 * (seed + 1), 400) == 0  # tight caps: growth
+        assert e.check() == ""
+        assert diff_states(o.export(), e.export()) == []

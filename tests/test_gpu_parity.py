@@ -13,6 +13,8 @@ import crdt_amd  # noqa: E402
 from crdt_amd.traces import load_remote_wire, load_trace  # noqa: E402
 from oracle_lib import OracleDoc  # noqa: E402
 from fuzz_gen import random_local_trace  # noqa: E402
+import sys, os  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))  # bench helpers
 
 KEYS = ("raw", "leaf_sizes", "canon", "cwo", "deletes", "dd", "txns", "parents", "frontier", "len", "next_order")
 
@@ -164,3 +166,25 @@ def test_concurrent_histories():
         if so == 0:
             assert int(dg[i]) == o.digest()
             assert_same(e.export(i), o.export())
+
+
+def _seed32(seed, doc):
+    from bench import splitmix64
+    return splitmix64(seed ^ doc) & 0xFFFFFFFF
+
+
+def test_generated_config4():
+    # BASELINE config 4 shape: every document's edit stream is generated on the device from one
+    # GEN record (make_random_change semantics, doc.rs:544-569), 20,000 ops per document.
+    n_docs, n_ops, seed = 96, 20000, 0xC0FFEE
+    e = crdt_amd.Engine(n_docs, 32)
+    st = e.apply_random(list(range(n_docs)), "gen", n_ops, seed)
+    assert (st == 0).all(), st
+    dg = e.digests()
+    for d in range(n_docs):
+        o = OracleDoc()
+        assert o.apply_random(o.agent("gen"), n_ops, _seed32(seed, d)) == 0
+        assert int(dg[d]) == o.digest(), d
+        if d < 3:
+            assert_same(e.export(d), o.export())
+            check_queries(e, d, o)

@@ -238,3 +238,15 @@ def test_queries_roundtrip():
     p3, dl3 = d.loc_to_pos(np.zeros_like(allseq, dtype=np.uint16), allseq)
     assert ((dl3 == 0) | (dl3 == 1) | (dl3 == 2)).all()
     assert (p3[dl3 != 2] <= len(d)).all()
+
+
+# --- config 4 generator: doc.rs:571-587 random_single_document invariants + distribution ------
+def test_generator_invariants():
+    d = OracleDoc()
+    a = d.agent("seph")
+    assert d.apply_random(a, 20000, 12345) == 0
+    s = d.sizes()
+    assert s["cwo"] == 1 and s["agents"] == 1 and s["txns"] == 1 and s["frontier"] == 1
+    # make_random_change keeps the document short (deletes of up to 10 chars outweigh inserts)
+    assert len(d) <= 200
+    assert s["next_order"] > 20000   # deletes of 1..10 chars consume several orders each

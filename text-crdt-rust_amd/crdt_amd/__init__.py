@@ -78,6 +78,7 @@ def lib():
     L.crdt_apply_remote_wire.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(u64), P(i32)]
     L.crdt_stage_remote_wire.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(u64)]
     L.crdt_stage_remote_replicated.argtypes = [vp, C.c_char_p, u64, u32, P(C.c_char_p)]
+    L.crdt_stage_random.argtypes = [vp, u64, P(u32), C.c_char_p, u32, u64]
     L.crdt_reset_async.argtypes = [vp]
     L.crdt_run.argtypes = [vp, P(i32)]
     L.crdt_run_async.argtypes = [vp]
@@ -106,7 +107,7 @@ EXPORTED_SYMBOLS = [
     "crdt_stage_remote_replicated", "crdt_reset_async", "crdt_run", "crdt_run_async", "crdt_publish_async",
     "crdt_sync", "crdt_pos_to_loc", "crdt_loc_to_pos", "crdt_pos_to_loc_dev_async", "crdt_loc_to_pos_dev_async",
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
-    "crdt_stream", "crdt_last_error",
+    "crdt_stream", "crdt_last_error", "crdt_stage_random",
 ]
 
 
@@ -211,6 +212,16 @@ class Engine:
     def stage_remote_replicated(self, wire: bytes, rename_idx: int, names: Sequence[str]):
         arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
         _check(self.L.crdt_stage_remote_replicated(self.h, wire, len(wire), rename_idx, arr), "stage_replicated")
+
+    # --- config 4: make_random_change (doc.rs:544-569) generated on the device
+    def stage_random(self, docs: Sequence[int], agent: str, n_ops: int, seed: int):
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        _check(self.L.crdt_stage_random(self.h, d.shape[0], _p(d), agent.encode(), n_ops, seed), "stage_random")
+
+    def apply_random(self, docs: Sequence[int], agent: str, n_ops: int, seed: int) -> np.ndarray:
+        self.stage_random(docs, agent, n_ops, seed)
+        st = self.run()
+        return st[np.asarray(docs, dtype=np.int64)]
 
     def reset_async(self):
         _check(self.L.crdt_reset_async(self.h), "reset")

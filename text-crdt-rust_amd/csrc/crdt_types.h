@@ -87,7 +87,7 @@ struct GroupRec { u32 blk, cnt, vis, pad; };   // persisted root level of the di
 // ---------------------------------------------------------------------------------------------
 // Op record stream (16 B records, per document, in causal order)
 // ---------------------------------------------------------------------------------------------
-enum : u32 { REC_LTXN = 1, REC_LOP = 2, REC_RTXN = 3, REC_RINS = 4, REC_RDEL = 5, REC_RPARENT = 6 };
+enum : u32 { REC_LTXN = 1, REC_LOP = 2, REC_RTXN = 3, REC_RINS = 4, REC_RDEL = 5, REC_RPARENT = 6, REC_GEN = 7 };
 struct Rec { u32 w0, w1, w2, w3; };
 // LTXN    w0 = kind<<28 | n_ops         w1 = agent                  w2 = sum(del) w3 = txn_len
 // LOP     w0 = kind<<28                 w1 = pos                    w2 = del   w3 = ins
@@ -96,8 +96,33 @@ struct Rec { u32 w0, w1, w2, w3; };
 // RINS    w0 = kind<<28 | len (28b)     w1 = ol_agent | or_agent<<16  w2 = ol_seq  w3 = or_seq
 // RDEL    w0 = kind<<28 | len (28b)     w1 = agent                  w2 = seq
 // RPARENT w0 = kind<<28                 w1 = agent                  w2 = seq
-// (remote ops follow their RTXN, then the txn's RPARENT records)
+// GEN     w0 = kind<<28                 w1 = agent                  w2 = n_ops w3 = seed
+// (remote ops follow their RTXN, then the txn's RPARENT records; a GEN record expands on the
+//  device into n_ops local txns of one LocalOp each, see gen_op)
 CRDT_HD u32 rec_kind(const Rec& r) { return r.w0 >> 28; }
+
+CRDT_HD u64 mix64(u64 z) {  // splitmix64 finaliser
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+// On-device edit generator (BASELINE config 4).  Semantics of the reference's
+// make_random_change (doc.rs:544-569): insert with probability 0.55 while len < 100, else 0.45
+// (always when empty); insert 1 char at U[0, len]; delete U[1, min(10, len - pos)] chars at
+// U[0, len - 1].  The reference's SmallRng stream is Rust-only, so draws come from a counter-based
+// hash of (seed, op#) with fixed-point thresholds: integer-exact on the device and in the oracle.
+// Returns the LOP record of op `i` for a document of visible length `len`.
+CRDT_HD Rec gen_op(u32 seed, u32 i, u32 len) {
+  u64 r = mix64(((u64)seed << 32) | i);
+  u32 hi = (u32)(r >> 32), lo = (u32)r;
+  u32 thr = len < 100u ? 0x8CCCCCCDu : 0x73333333u;  // 0.55 / 0.45 of 2^32
+  if (len == 0u || hi < thr) return Rec{REC_LOP << 28, (u32)(((u64)lo * (len + 1u)) >> 32), 0u, 1u};
+  u32 p = (u32)(((u64)lo * len) >> 32);
+  u32 mx = len - p < 10u ? len - p : 10u;
+  u32 r2 = (u32)mix64(r);
+  return Rec{REC_LOP << 28, p, 1u + (u32)(((u64)r2 * mx) >> 32), 0u};
+}
 
 // ---------------------------------------------------------------------------------------------
 // Per-document segments (host-assigned, read-only during replay) and mutable header
@@ -122,7 +147,7 @@ struct DocState {
   u32 ng, next_order, len, n_cwo;
   u32 n_del, n_dd, n_txn, n_par;
   u32 n_fr, n_agents, n_items, cap_need;
-  u32 n_entries, pad0, pad1, pad2;
+  u32 n_entries, gen_done, pad1, pad2;  // gen_done: ops of the current GEN record applied
 };
 
 struct Pools {

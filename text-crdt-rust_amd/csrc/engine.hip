@@ -324,25 +324,47 @@ struct crdt_engine {
       HIPCHK(dalloc(recs, rec_cap));
     }
     for (auto& sg : seg_h) { sg.rec_base = 0; sg.rec_n = 0; }
+    // Consecutive distinct streams go up in one host->device copy; a replicated stream (same
+    // host vector as the previous document) is a device-to-device copy of that upload.
     u64 off = 0;
     const std::vector<Rec>* prev = nullptr;
     u64 prev_off = 0;
+    std::vector<Rec> hb;
+    u64 hb_off = 0;
+    auto flush = [&]() -> int {
+      if (hb.empty()) return 0;
+      HIPCHK(hipMemcpyAsync(recs + hb_off, hb.data(), hb.size() * sizeof(Rec), hipMemcpyHostToDevice, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+      hb.clear();
+      return 0;
+    };
     for (size_t i = 0; i < doc_ids.size(); i++) {
       DocSeg& sg = seg_h[doc_ids[i]];
       const std::vector<Rec>& sv = *streams[i];
       sg.rec_base = off;
       sg.rec_n = (u32)sv.size();
       if (!sv.empty()) {
-        if (&sv == prev)  // replicated stream: device-to-device copy of the previous upload
+        if (&sv == prev) {
+          r = flush();
+          if (r) return r;
           HIPCHK(hipMemcpyAsync(recs + off, recs + prev_off, sv.size() * sizeof(Rec), hipMemcpyDeviceToDevice, stream));
-        else
+        } else if (sv.size() > (1u << 20)) {  // large stream: straight from the caller's vector
+          r = flush();
+          if (r) return r;
           HIPCHK(hipMemcpyAsync(recs + off, sv.data(), sv.size() * sizeof(Rec), hipMemcpyHostToDevice, stream));
-        HIPCHK(hipStreamSynchronize(stream));
+          HIPCHK(hipStreamSynchronize(stream));
+        } else {
+          if (hb.empty()) hb_off = off;
+          hb.insert(hb.end(), sv.begin(), sv.end());
+        }
       }
       prev = &sv;
       prev_off = off;
       off += sv.size();
     }
+    r = flush();
+    if (r) return r;
+    HIPCHK(hipStreamSynchronize(stream));
     if (grow) {
       r = layout(true);
       if (r) return r;
@@ -585,6 +607,23 @@ int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t w
     encode_remote(uniq.back(), needs[d], at, w2);
     sp[d] = &uniq.back();
     if (d == 0) for (const auto& n : w2.names) first_map.push_back(at.lookup(n));
+  }
+  return e->stage(ids, sp, needs);
+}
+
+int crdt_stage_random(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const char* agent, uint32_t n_ops,
+                      uint64_t seed) {
+  if (!valid(e) || !docs || !agent || n_ops == 0 || std::strcmp(agent, "ROOT") == 0) return CRDT_E_ARG;
+  std::vector<u64> ids(n_docs);
+  std::vector<std::vector<Rec>> streams(n_docs);
+  std::vector<StreamNeeds> needs(n_docs);
+  std::vector<const std::vector<Rec>*> sp(n_docs);
+  for (uint64_t i = 0; i < n_docs; i++) {
+    if (docs[i] >= e->n_docs) return CRDT_E_ARG;
+    ids[i] = docs[i];
+    u32 a = e->docs[docs[i]].agents.get_or_create(agent);
+    encode_gen(streams[i], needs[i], a, n_ops, (u32)mix64(seed ^ docs[i]));
+    sp[i] = &streams[i];
   }
   return e->stage(ids, sp, needs);
 }

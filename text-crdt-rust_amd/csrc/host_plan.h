@@ -166,6 +166,22 @@ inline void encode_remote(std::vector<Rec>& out, StreamNeeds& nd, AgentTable& at
   }
 }
 
+// One GEN record: `n_ops` local txns of one generated LocalOp each (gen_op, on the device).
+// Orders and delete runs are estimates (about 2.8 orders per op for make_random_change's
+// distribution); a table that fills stops the document resumably and grows.
+inline void encode_gen(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, u32 n_ops, u32 seed) {
+  out.push_back(Rec{REC_GEN << 28, agent, n_ops, seed});
+  nd.n_txn += n_ops;
+  nd.n_ltxn += n_ops;
+  nd.n_ops += n_ops;
+  nd.orders += 3ull * n_ops;
+  nd.local_del += n_ops;
+  if (agent < 0xFFFE) {
+    if (nd.txns_per_agent.size() <= agent) nd.txns_per_agent.resize(agent + 1, 0);
+    nd.txns_per_agent[agent] += n_ops;
+  }
+}
+
 // Capacities for a fresh document that will apply `nd` (heuristic leaf capacity; everything
 // else is an upper bound).  Growth for leaves/blocks is handled by the caller on ST_CAPACITY.
 constexpr u32 MAX_LEAVES = 32 * (MAX_GROUPS - 1);  // root level holds <= MAX_GROUPS blocks

@@ -103,12 +103,6 @@ __global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const Do
 // ---------------------------------------------------------------------------------------------
 // digest helpers (identical to oracle/crdt_oracle.hpp)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ u64 mix64(u64 z) {
-  z += 0x9E3779B97F4A7C15ull;
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
 __device__ __forceinline__ u64 elem_hash(u32 section, u64 idx, u64 a, u64 b) {
   u64 k = mix64(((u64)section << 56) ^ idx);
   return mix64(mix64(k ^ a) ^ b);

@@ -54,7 +54,7 @@ enum : u32 {
   // DocState, field for field (struct order, 20 dwords)
   S_BASE = 40,
   S_STATUS = 40, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
-  S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES,
+  S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES, S_GEN_DONE,
   // leaf cache bookkeeping
   C_LEAF = 64, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
@@ -68,7 +68,7 @@ enum : u32 {
   T_RB_BASE,
   N_SLOTS
 };
-static_assert(S_N_ENTRIES - S_BASE + 4 == sizeof(DocState) / 4, "DocState slot mirror");
+static_assert(S_GEN_DONE - S_BASE + 3 == sizeof(DocState) / 4, "DocState slot mirror");
 static_assert(N_SLOTS <= 128, "two context registers");
 
 template <class W, int L>
@@ -171,6 +171,7 @@ struct Replayer {
     p(S_N_ITEMS, 0);
     p(S_CAP_NEED, 0);
     p(S_N_ENTRIES, 0);
+    p(S_GEN_DONE, 0);
     w.zero_leaf(leafp(0), L);
     w.st(dl(), 0u);
     w.st(dv(), 0u);
@@ -824,7 +825,8 @@ struct Replayer {
 
   // One txn: doc.rs:376-469 apply_local_txn (remote = false) or doc.rs:242-348
   // apply_remote_txn (remote = true).  Header at record `pos`; ops (then parents) follow.
-  CRDT_HD i32 apply_txn(const Rec& h, u32 pos, bool remote) {
+  // gen: the txn comes from a GEN record; its single LocalOp is `gop` (no op record to read).
+  CRDT_HD i32 apply_txn(const Rec& h, u32 pos, bool remote, u32 gen, const Rec& gop) {
     u32 nops, agent, np = 0, seq, txn_len;
     if (!remote) {
       nops = h.w0 & 0x0FFFFFFFu;
@@ -860,7 +862,7 @@ struct Replayer {
       // ---------------------------------------------------------------- next op
       if (mode == M_FETCH) {
         if (k == nops) break;
-        Rec op = rec(pos + 1 + k);
+        Rec op = gen ? gop : rec(pos + 1 + k);
         k++;
         if (!remote) {  // LocalOp: delete (visible range) first, then insert (doc.rs:386-465)
           lpos = op.w1;
@@ -1181,28 +1183,39 @@ struct Replayer {
     return fast_delete(idx, off, l, first) ? per : 0u;
   }
 
-  // Replay this document's record stream from its rec_pos.
+  // Replay this document's record stream from its rec_pos.  A GEN record stays current until
+  // all its ops are applied (progress in S_GEN_DONE, so a capacity stop resumes mid-record).
   CRDT_HD void run() {
     u32 pos = g(S_REC_POS);
     u32 rn = rec_n();
     while (pos < rn) {
       Rec h = rec(pos);
       u32 kind = rec_kind(h);
+      u32 gen = kind == REC_GEN;
+      Rec gop{0, 0, 0, 0};
+      if (gen) {
+        u32 done = g(S_GEN_DONE);
+        if (done >= h.w2) { p(S_GEN_DONE, 0); pos += 1; continue; }
+        gop = gen_op(h.w3, done, cur_len());
+        h = Rec{(REC_LTXN << 28) | 1u, h.w1, gop.w2, gop.w2 + gop.w3};
+        kind = REC_LTXN;
+      }
       i32 st;
       u32 consumed;
       if (kind == REC_LTXN || kind == REC_RTXN) {
-        u32 fast = fast_txn(pos, kind);
+        u32 fast = gen ? 0u : fast_txn(pos, kind);
         if (fast) { pos += fast; continue; }
         bool remote = kind == REC_RTXN;
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
-        consumed = 1 + nops + (remote ? (h.w1 >> 16) : 0u);
-        st = (pos + consumed <= rn) ? apply_txn(h, pos, remote) : ST_BAD_INPUT;
+        consumed = gen ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
+        st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, gen, gop) : ST_BAD_INPUT;
       } else {
         st = ST_BAD_INPUT;
         consumed = 1;
       }
       if (st == ST_NEED_CAPACITY) { p(S_STATUS, (u32)st); break; }  // resumable at `pos` after growth
       if (st != ST_OK) { p(S_STATUS, (u32)st); pos += consumed; break; }
+      if (gen) { inc(S_GEN_DONE); continue; }
       pos += consumed;
     }
     p(S_REC_POS, pos);
