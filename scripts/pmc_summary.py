@@ -6,7 +6,7 @@ agg = {}
 for f in sorted(glob.glob("gpurun_out/pmc*/**/*counter_collection.csv", recursive=True)):
     last = {}
     for r in csv.DictReader(open(f)):
-        if "k_replay" not in r["Kernel_Name"]:
+        if not r.get("Kernel_Name") or "k_replay" not in r["Kernel_Name"]:
             continue
         key = r["Counter_Name"]
         did = int(r["Dispatch_Id"])

@@ -139,6 +139,30 @@ struct WaveCPU {
     return n;
   }
 
+  u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 delta) const {
+    u32 per = remote ? 3u : 2u;
+    u32 n = 1;
+    for (u32 j = b0 + per; j + per <= nv; j += per) {
+      const Rec &h = rb[j], &o = rb[j + 1], &ph = rb[j - per], &po = rb[j - per + 1];
+      bool ok;
+      if (remote) {
+        const Rec& pr = rb[j + 2];
+        ok = h.w0 == ((REC_RTXN << 28) | 1u) && h.w1 == (agent | (1u << 16)) && h.w2 == ph.w2 + 1u && h.w3 == 1u &&
+             o.w0 == ((REC_RDEL << 28) | 1u) && o.w1 == agent && o.w2 == po.w2 + delta &&
+             pr.w0 == (REC_RPARENT << 28) && pr.w1 == agent && pr.w2 == h.w2 - 1u;
+      } else {
+        ok = h.w0 == ((REC_LTXN << 28) | 1u) && h.w1 == agent && h.w2 == 1u && h.w3 == 1u &&
+             o.w0 == (REC_LOP << 28) && o.w2 == 1u && o.w3 == 0u && o.w1 == po.w1 + delta;
+      }
+      if (!ok) break;
+      n++;
+    }
+    return n;
+  }
+  void st_del_run(DelRun* p, u32 cnt, u32 key0, u32 t0) const {
+    for (u32 j = 0; j < cnt; j++) p[j] = DelRun{key0 + j, t0 - j, 1u};
+  }
+
   // directory root
   void root_init(u32 blk, u32 cnt, u32 vis) {
     std::memset(gb, 0, sizeof(gb)); std::memset(gc, 0, sizeof(gc)); std::memset(gv, 0, sizeof(gv));

@@ -1079,9 +1079,8 @@ struct Replayer {
   }
   // Delete `l` items at offset `off` of visible entry idx of the cached leaf: mutate_entry
   // (mutations.rs:227-277) and insert_internal's prepend / shift (mutations.rs:84-146) without a
-  // leaf split.  Returns 0, having changed nothing, when a split or a table growth is needed.
-  CRDT_HD u32 fast_delete(u32 idx, u32 off, u32 l, u32 first) {
-    if ((g(K_MAP) - first < l) | (g(K_DEL) == g(S_N_DEL))) return 0;
+  // leaf split.  Returns 0, having changed nothing, when the leaf has no room.
+  CRDT_HD u32 leaf_delete(u32 idx, u32 off, u32 l) {
     Span e = w.cget(idx);
     u32 n = g(C_N);
     u32 target = e.order + off;
@@ -1113,10 +1112,63 @@ struct Replayer {
       if (m == 2u) set(idx + 2u, pc);
       inc(S_N_ENTRIES, m);
     }
-    append_delete(first, target, l);    // doc.rs:305-308 / 420-423
-    w.fill(lof() + first, l, INVALID);  // delete orders name no item
-    fast_txn_commit(first, l);
     return 1;
+  }
+  // Delete txns: the one at b0 (l items at `off` of entry idx) and, when it deletes one item, the
+  // run of one-item delete txns that follows it in the prefetch block -- backspacing (each
+  // deletes the item before the previous one) or forward deleting (the item after) -- validated
+  // lane-parallel (W::delete_scan).  Each delete is applied to the leaf exactly as apply_txn
+  // would (leaf_delete); the RLE tables, the order map and the txn log are updated once for the
+  // run.  Returns records consumed (0: nothing applied).
+  CRDT_HD u32 fast_deletes(u32 b0, u32 nv, u32 remote, u32 agent, u32 idx, u32 off, u32 l, u32 first, const Rec& o) {
+    u32 per = remote ? 3u : 2u;
+    u32 t1 = w.cget_order(idx) + off;
+    u32 k = 1, back = 0;
+    u32 key = g(T_AGL_KEY);
+    u32 in_run = !remote || (((o.w1 & 0xFFFFu) == agent) & (o.w2 - key < g(T_AGL_LEN)));
+    if ((l == 1u) & (b0 + 2u * per <= nv) & in_run) {
+      Rec o2 = w.rec_get(b0 + per + 1u);
+      u32 delta = remote ? o2.w2 - o.w2 : o2.w1 - o.w1;
+      back = delta == 0xFFFFFFFFu;
+      u32 fwd = delta == (remote ? 1u : 0u);
+      if (back | fwd) {
+        k = w.delete_scan(b0, nv, remote, agent, delta);
+        u32 room = back ? off + 1u : (u32)w.cget_len(idx) - off;  // targets stay in this entry
+        if (remote) {  // ... and in the author's last item_orders run (contiguous orders)
+          u32 r2 = back ? o.w2 - key + 1u : key + g(T_AGL_LEN) - o.w2;
+          room = room < r2 ? room : r2;
+        }
+        k = k < room ? k : room;
+      }
+    }
+    if ((g(K_MAP) - first < k * l) | (g(K_DEL) - g(S_N_DEL) < k)) return 0;
+    u32 done = 0;
+    for (u32 j = 0; j < k; j++) {
+      u32 ij = back ? idx : (j == 0u ? idx : idx + (off > 0u) + j);  // forward: the remainder moves right
+      u32 oj = back ? off - j : (j == 0u ? off : 0u);
+      u32 tj = back ? t1 - j : t1 + j;
+      if ((w.cget_order(ij) + oj != tj) | (w.cget_len(ij) <= (i32)oj)) break;
+      if (!leaf_delete(ij, oj, l)) break;
+      done++;
+    }
+    if (done == 0u) return 0;
+    if (back) {  // doc.rs:305-308 / 420-423: backspaced targets never coalesce: one run each
+      append_delete(first, t1, 1u);
+      if (done > 1u) {
+        u32 n = g(S_N_DEL);
+        w.st(&dels()[n - 1u].len, g(T_DEL_LEN));  // retire the tail
+        w.st_del_run(dels() + n, done - 1u, first + 1u, t1 - 1u);
+        p(S_N_DEL, n + done - 1u);
+        p(T_DEL_KEY, first + done - 1u);
+        p(T_DEL_ORDER, t1 - (done - 1u));
+        p(T_DEL_LEN, 1u);
+      }
+    } else {
+      append_delete(first, t1, done * l);  // forward deletes coalesce into one run (Rle::append)
+    }
+    w.fill(lof() + first, done * l, INVALID);  // delete orders name no item
+    fast_txn_commit(first, done * l);
+    return done * per;
   }
   // Returns the records consumed by a fast-path txn at `pos`, or 0 (use apply_txn).
   CRDT_HD u32 fast_txn(u32 pos, u32 kind) {
@@ -1135,10 +1187,11 @@ struct Replayer {
     nv = nv < 64u ? nv : 64u;
     Rec h = w.rec_get(b0), o = w.rec_get(b0 + 1u);
     u32 first = g(S_NEXT_ORDER);
-    u32 idx, off, l;
+    u32 idx, off, l, agent;
     if (remote) {
       Rec pr = w.rec_get(b0 + 2u);
-      u32 agent = h.w1 & 0xFFFFu, seq = h.w2;
+      agent = h.w1 & 0xFFFFu;
+      u32 seq = h.w2;
       l = o.w0 & 0x0FFFFFFFu;
       u32 ok = (h.w0 == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
                (pr.w0 == (REC_RPARENT << 28)) & (pr.w1 == agent) & (pr.w2 == seq - 1u);
@@ -1163,7 +1216,8 @@ struct Replayer {
       off = target - w.cget_order(idx);
       if ((el <= 0) | (off + l > (u32)el)) return 0;  // already deleted / spans entries
     } else {
-      u32 agent = h.w1, lp = o.w1, del = o.w2, ins = o.w3;
+      agent = h.w1;
+      u32 lp = o.w1, del = o.w2, ins = o.w3;
       l = del + ins;
       u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l) &
                ((del == 0u) != (ins == 0u)) & (l - 1u < 0xFFFFu) & (g(C_VS_OK) != 0u) & ((ins == 0u) | (lp != 0u));
@@ -1180,7 +1234,7 @@ struct Replayer {
       }
       if (off + l > (u32)el) return 0;
     }
-    return fast_delete(idx, off, l, first) ? per : 0u;
+    return fast_deletes(b0, nv, remote, agent, idx, off, l, first, o);
   }
 
   // Replay this document's record stream from its rec_pos.  A GEN record stays current until

@@ -294,6 +294,44 @@ struct WaveGPU {
     return n;
   }
 
+  // Delete-run scan (replay_core.h fast_deletes): lane k checks record k against "one-item delete
+  // txn continuing the previous one" -- remote: RTXN{1 op, 1 parent} of length 1, seq = previous
+  // seq + 1, RDEL of 1 item of `agent` at the previous target seq + delta, RPARENT (agent, seq-1);
+  // local: LTXN{1 op} deleting 1 item at the previous pos + delta.  Returns the run length in
+  // txns (>= 1; the txn at b0 was checked by the caller).
+  __device__ __forceinline__ u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 delta) const {
+    u32 l = lane_id();
+    u32 rel = l - b0;
+    u32 per = remote ? 3u : 2u;
+    u32 t = remote ? (rel * 43u) >> 7 : rel >> 1;
+    u32 r = rel - t * per;
+    bool ok;
+    if (remote) {
+      u32 ps = shfl(rz, r == 2u ? l - 2u : l - 3u);  // previous header / previous op / own header
+      bool okh = rx == ((REC_RTXN << 28) | 1u) && ry == (agent | (1u << 16)) && rz == ps + 1u && rw == 1u;
+      bool oko = rx == ((REC_RDEL << 28) | 1u) && ry == agent && rz == ps + delta;
+      bool okp = rx == (REC_RPARENT << 28) && ry == agent && rz == ps - 1u;
+      ok = r == 0u ? okh : (r == 1u ? oko : okp);
+    } else {
+      u32 pp = shfl(ry, l - 2u);  // previous op's pos
+      bool okh = rx == ((REC_LTXN << 28) | 1u) && ry == agent && rz == 1u && rw == 1u;
+      bool oko = rx == (REC_LOP << 28) && rz == 1u && rw == 0u && ry == pp + delta;
+      ok = r == 0u ? okh : oko;
+    }
+    u64 stop = ballot(l >= b0 + per && (!ok || l >= nv));
+    u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
+    return remote ? ((f - b0) * 43u) >> 7 : (f - b0) >> 1;
+  }
+  // runs {key0 + j, t0 - j, 1} for j < cnt (backspaced deletes), lane-parallel
+  __device__ __forceinline__ void st_del_run(DelRun* p, u32 cnt, u32 key0, u32 t0) const {
+    for (u32 j = lane_id(); j < cnt; j += 64) {
+      u32* q = (u32*)(p + j);
+      q[0] = key0 + j;
+      q[1] = t0 - j;
+      q[2] = 1u;
+    }
+  }
+
   // ---------------------------------------------------------------- directory root (VGPRs)
   __device__ __forceinline__ u32* rblk() const { return rt; }
   __device__ __forceinline__ u32* rcnt() const { return rt + MAX_GROUPS; }
