@@ -24,6 +24,7 @@ struct WaveCPU {
   void x_load_state(const DocState* p, u32 base) { std::memcpy(x + base, p, sizeof(DocState)); }
   void x_store_state(DocState* p, u32 base) const { std::memcpy(p, x + base, sizeof(DocState)); }
 
+  static u64 clock() { return 0; }
   u32 ld(const u32* p) const { return *p; }
   void st(u32* p, u32 v) const { *p = v; }
   void st(i32* p, i32 v) const { *p = v; }
@@ -112,8 +113,17 @@ struct WaveCPU {
     for (i32 i = (i32)n - 1; i >= (i32)idx; i--) c[i + k] = c[i];
     for (u32 i = idx; i < idx + k; i++) c[i] = Span{0, 0, 0, 0};
   }
-  Rec rb[64];
-  void rec_block_load(const Rec* p, u32 n) { for (u32 i = 0; i < n; i++) rb[i] = p[i]; }
+  Rec rb[64], qb[64];
+  void rec_load2(const Rec* p, u32 n, u32 n_ahead) {
+    for (u32 i = 0; i < n; i++) rb[i] = p[i];
+    for (u32 i = 0; i < n_ahead; i++) qb[i] = p[64 + i];
+  }
+  void rec_slide(u32 d, const Rec* p_ahead, u32 n_ahead) {
+    Rec t[128];
+    for (u32 i = 0; i < 64; i++) { t[i] = rb[i]; t[64 + i] = qb[i]; }
+    for (u32 i = 0; i < 64; i++) rb[i] = t[(i + d) & 127];
+    for (u32 i = 0; i < n_ahead; i++) qb[i] = p_ahead[i];
+  }
   Rec rec_get(u32 k) const { return rb[k]; }
   u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 ow1, u32 ow3, u32& total) const {
     u32 per = remote ? 3u : 2u;

@@ -33,22 +33,23 @@ class CrdtError(RuntimeError):
     pass
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile libcrdt_gpu.so for gfx950 with hipcc (in-tree)."""
+def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defines: Sequence[str] = ()) -> str:
+    """Compile libcrdt_gpu.so for gfx950 with hipcc (in-tree).  `defines` only for diagnostic
+    builds written to another `out` (e.g. CRDT_PROF)."""
     srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "crdt_gpu.h")]
-    if not force and os.path.exists(LIB_PATH):
-        lt = os.path.getmtime(LIB_PATH)
+    if not force and os.path.exists(out):
+        lt = os.path.getmtime(out)
         if all(os.path.getmtime(s) <= lt for s in srcs):
-            return LIB_PATH
-    os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
+            return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-fno-strict-aliasing", "-I" + INCLUDE, "-I" + CSRC, "-o", LIB_PATH + ".tmp",
+           "-fno-strict-aliasing", "-I" + INCLUDE, "-I" + CSRC, "-o", out + ".tmp"] + ["-D" + d for d in defines] + [
            os.path.join(CSRC, "engine.hip")]
     r = subprocess.run(cmd, capture_output=not verbose, text=True)
     if r.returncode != 0:
         raise CrdtError("hipcc failed:\n" + (r.stderr or "")[-4000:])
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(out + ".tmp", out)
+    return out
 
 
 _lib = None
@@ -58,9 +59,10 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise CrdtError(f"{LIB_PATH} not built (run __graft_entry__.build())")
-    L = C.CDLL(LIB_PATH)
+    path = os.environ.get("CRDT_GPU_LIB", LIB_PATH)  # diagnostic builds only (e.g. -DCRDT_PROF)
+    if not os.path.exists(path):
+        raise CrdtError(f"{path} not built (run __graft_entry__.build())")
+    L = C.CDLL(path)
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     P = C.POINTER
 
@@ -79,6 +81,7 @@ def lib():
     L.crdt_stage_remote_wire.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(u64)]
     L.crdt_stage_remote_replicated.argtypes = [vp, C.c_char_p, u64, u32, P(C.c_char_p)]
     L.crdt_stage_random.argtypes = [vp, u64, P(u32), C.c_char_p, u32, u64]
+    L.crdt_debug_state.argtypes = [vp, u32, P(u32)]
     L.crdt_reset_async.argtypes = [vp]
     L.crdt_run.argtypes = [vp, P(i32)]
     L.crdt_run_async.argtypes = [vp]
@@ -107,7 +110,7 @@ EXPORTED_SYMBOLS = [
     "crdt_stage_remote_replicated", "crdt_reset_async", "crdt_run", "crdt_run_async", "crdt_publish_async",
     "crdt_sync", "crdt_pos_to_loc", "crdt_loc_to_pos", "crdt_pos_to_loc_dev_async", "crdt_loc_to_pos_dev_async",
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
-    "crdt_stream", "crdt_last_error", "crdt_stage_random",
+    "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
 ]
 
 
@@ -222,6 +225,11 @@ class Engine:
         self.stage_random(docs, agent, n_ops, seed)
         st = self.run()
         return st[np.asarray(docs, dtype=np.int64)]
+
+    def debug_state(self, doc: int) -> np.ndarray:
+        out = np.zeros(20, np.uint32)
+        _check(self.L.crdt_debug_state(self.h, doc, _p(out)), "debug_state")
+        return out
 
     def reset_async(self):
         _check(self.L.crdt_reset_async(self.h), "reset")

@@ -55,6 +55,7 @@ enum : u32 {
   S_BASE = 40,
   S_STATUS = 40, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
   S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES, S_GEN_DONE,
+  S_PROF0, S_PROF1,  // diagnostic builds (-DCRDT_PROF): cycles in fast paths / general interpreter
   // leaf cache bookkeeping
   C_LEAF = 64, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
@@ -68,7 +69,7 @@ enum : u32 {
   T_RB_BASE,
   N_SLOTS
 };
-static_assert(S_GEN_DONE - S_BASE + 3 == sizeof(DocState) / 4, "DocState slot mirror");
+static_assert(S_PROF1 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
 static_assert(N_SLOTS <= 128, "two context registers");
 
 template <class W, int L>
@@ -221,15 +222,22 @@ struct Replayer {
   }
 
   // ------------------------------------------------------------------ records
+  // The op stream is read through a 64-record window [T_RB_BASE, +64) in VGPR lanes plus the
+  // following 64 records, loaded ahead asynchronously: moving the window forward by d <= 64
+  // slides it over the block ahead with lane shuffles and only issues the next block's load, so
+  // the replay almost never waits for a record load.
+  CRDT_HD void rec_window(u32 base) {
+    u32 d = base - g(T_RB_BASE);
+    u32 nn = rec_n() - base;
+    u32 ahead = nn > 64u ? nn - 64u : 0u;
+    if (d <= 64u) w.rec_slide(d, recs() + base + 64u, ahead < 64u ? ahead : 64u);
+    else w.rec_load2(recs() + base, nn < 64u ? nn : 64u, ahead < 64u ? ahead : 64u);
+    p(T_RB_BASE, base);
+  }
   CRDT_HD Rec rec(u32 pos) {
-    u32 rb = g(T_RB_BASE);
-    if (pos - rb >= 64u) {
-      rb = pos;
-      p(T_RB_BASE, pos);
-      u32 n = rec_n() - pos;
-      w.rec_block_load(recs() + pos, n < 64u ? n : 64u);
-    }
-    return w.rec_get(pos - rb);
+    u32 d = pos - g(T_RB_BASE);
+    if (d >= 64u) rec_window(d < 128u ? g(T_RB_BASE) + 64u : pos);
+    return w.rec_get(pos - g(T_RB_BASE));
   }
 
   // ------------------------------------------------------------------ directory
@@ -1177,10 +1185,8 @@ struct Replayer {
     u32 rn = rec_n();
     if ((rn - pos < per) | (g(C_LEAF) == INVALID)) return 0;
     u32 b0 = pos - g(T_RB_BASE);
-    if (b0 + per > 64u) {  // re-base the prefetch block: the txn and what follows it
-      u32 nn = rn - pos;
-      p(T_RB_BASE, pos);
-      w.rec_block_load(recs() + pos, nn < 64u ? nn : 64u);
+    if (b0 + per > 64u) {  // move the window to the txn (and what follows it)
+      rec_window(pos);
       b0 = 0;
     }
     u32 nv = rn - g(T_RB_BASE);
@@ -1257,12 +1263,23 @@ struct Replayer {
       i32 st;
       u32 consumed;
       if (kind == REC_LTXN || kind == REC_RTXN) {
+#ifdef CRDT_PROF
+        u64 t0 = w.clock();
+#endif
         u32 fast = gen ? 0u : fast_txn(pos, kind);
+#ifdef CRDT_PROF
+        u64 t1 = w.clock();
+        if (fast) inc(S_PROF0, (u32)(t1 - t0));
+        else inc(S_PROF1, (u32)(t1 - t0));
+#endif
         if (fast) { pos += fast; continue; }
         bool remote = kind == REC_RTXN;
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
         consumed = gen ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, gen, gop) : ST_BAD_INPUT;
+#ifdef CRDT_PROF
+        inc(S_PROF1, (u32)(w.clock() - t1));
+#endif
       } else {
         st = ST_BAD_INPUT;
         consumed = 1;

@@ -62,6 +62,8 @@ struct WaveGPU {
     if (l >= base && l < base + (u32)(sizeof(DocState) / 4)) q[l - base] = x0;
   }
 
+  __device__ __forceinline__ static u64 clock() { return __builtin_amdgcn_s_memtime(); }
+
   // ---------------------------------------------------------------- leaf cache
   u32 eo = 0, el = 0, er = 0;
   i32 en = 0;
@@ -251,12 +253,40 @@ struct WaveGPU {
     en = mv ? (i32)c : (z ? 0 : en);
   }
 
-  // ---------------------------------------------------------------- record prefetch (64 per load)
-  u32 rx = 0, ry = 0, rz = 0, rw = 0;
-  __device__ __forceinline__ void rec_block_load(const Rec* p, u32 n) {
+  // ---------------------------------------------------------------- record window (64 + 64 ahead)
+  u32 rx = 0, ry = 0, rz = 0, rw = 0;  // window: lane k = record base + k
+  u32 qx = 0, qy = 0, qz = 0, qw = 0;  // next 64 records, loaded ahead
+  __device__ __forceinline__ static uint4 rec_lane_load(const Rec* p, u32 n) {  // n >= 1
     u32 l = lane_id();
-    uint4 v = *(const uint4*)(p + (l < n ? l : n - 1));  // n >= 1
+    return *(const uint4*)(p + (l < n ? l : n - 1));
+  }
+  __device__ __forceinline__ void rec_load2(const Rec* p, u32 n, u32 n_ahead) {
+    uint4 v = rec_lane_load(p, n);
     rx = v.x; ry = v.y; rz = v.z; rw = v.w;
+    if (n_ahead) {
+      uint4 q = rec_lane_load(p + 64, n_ahead);
+      qx = q.x; qy = q.y; qz = q.z; qw = q.w;
+    }
+  }
+  // window += d (d <= 64): lanes take records from the window or the block ahead; then load the
+  // block after the new window (n_ahead records at p_ahead) ahead
+  __device__ __forceinline__ void rec_slide(u32 d, const Rec* p_ahead, u32 n_ahead) {
+    if (d >= 64u) {
+      rx = qx; ry = qy; rz = qz; rw = qw;
+      d -= 64u;
+    }
+    if (d) {
+      u32 l = lane_id();
+      u32 src = (l + d) & 63u;
+      bool own = l + d < 64u;
+      u32 ax = shfl(rx, src), ay = shfl(ry, src), az = shfl(rz, src), aw = shfl(rw, src);
+      u32 bx = shfl(qx, src), by = shfl(qy, src), bz = shfl(qz, src), bw = shfl(qw, src);
+      rx = own ? ax : bx; ry = own ? ay : by; rz = own ? az : bz; rw = own ? aw : bw;
+    }
+    if (n_ahead) {
+      uint4 q = rec_lane_load(p_ahead, n_ahead);
+      qx = q.x; qy = q.y; qz = q.z; qw = q.w;
+    }
   }
   __device__ __forceinline__ Rec rec_get(u32 k) const {
     return Rec{rdlane(rx, k), rdlane(ry, k), rdlane(rz, k), rdlane(rw, k)};
