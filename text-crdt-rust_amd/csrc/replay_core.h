@@ -1178,6 +1178,32 @@ struct Replayer {
     fast_txn_commit(first, done * l);
     return done * per;
   }
+  // Insert one item run right after the cursor (idx, off), 0 < off <= |entry|, when integrate
+  // stops at once and the run cannot be appended: insert_internal (mutations.rs:17-179) splits
+  // the entry at the cursor (remainder after the item) and makes room, without a leaf split.
+  // Returns 0, having changed nothing, when the leaf or the order map has no room.
+  CRDT_HD u32 leaf_insert(u32 idx, u32 off, const Span& item) {
+    Span e = w.cget(idx);
+    u32 n = g(C_N);
+    u32 len = (u32)item.len;
+    u32 has_rem = off < slen(e);
+    u32 space = 1u + has_rem;
+    if ((n + space > (u32)L) | (g(K_MAP) - item.order < len)) return 0;
+    if (has_rem) {
+      Span rem = truncate(e, off);
+      set(idx, e);
+      w.cache_shift_right(idx + 1u, n, 2u);
+      set(idx + 2u, rem);
+    } else {
+      w.cache_shift_right(idx + 1u, n, 1u);
+    }
+    p(C_N, n + space);
+    inc(S_N_ENTRIES, space);
+    w.fill(lof() + item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
+    set(idx + 1u, item);
+    inc(S_N_ITEMS, len);
+    return 1;
+  }
   // Returns the records consumed by a fast-path txn at `pos`, or 0 (use apply_txn).
   CRDT_HD u32 fast_txn(u32 pos, u32 kind) {
     u32 remote = kind == REC_RTXN;
@@ -1193,54 +1219,54 @@ struct Replayer {
     nv = nv < 64u ? nv : 64u;
     Rec h = w.rec_get(b0), o = w.rec_get(b0 + 1u);
     u32 first = g(S_NEXT_ORDER);
-    u32 idx, off, l, agent;
+    u32 agent, l, ins, ol = 0, orr = ROOT_ORDER;
+    Cursor c;
     if (remote) {
       Rec pr = w.rec_get(b0 + 2u);
       agent = h.w1 & 0xFFFFu;
       u32 seq = h.w2;
       l = o.w0 & 0x0FFFFFFFu;
-      u32 ok = (h.w0 == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
-               (pr.w0 == (REC_RPARENT << 28)) & (pr.w1 == agent) & (pr.w2 == seq - 1u);
-      if (!ok || !fast_txn_ok(agent, seq, first)) return 0;
       u32 k = rec_kind(o);
-      if (k == REC_RINS) {
-        if (!(((o.w1 & 0xFFFFu) == agent) & (o.w2 == seq - 1u))) return 0;  // origin_left = first - 1
-        u32 orr;
-        if (id_to_order(o.w1 >> 16, o.w3, orr) != ST_OK) return 0;
-        i32 x = w.cfind_order(g(C_N), first - 1u);
-        if (x < 0) return 0;
-        u32 nxo, has = next_item_after((u32)x, nxo);
-        if (has && nxo != orr) return 0;  // integrate would scan (doc.rs:183-221)
-        return fast_typing(b0, nv, 1u, (u32)x, orr, agent, o, first);
-      }
-      u32 target;
-      if (k != REC_RDEL || id_to_order(o.w1 & 0xFFFFu, o.w2, target) != ST_OK || target == ROOT_ORDER) return 0;
-      i32 x = w.cfind_order(g(C_N), target);
-      if (x < 0) return 0;
-      idx = (u32)x;
-      i32 el = w.cget_len(idx);
-      off = target - w.cget_order(idx);
-      if ((el <= 0) | (off + l > (u32)el)) return 0;  // already deleted / spans entries
+      ins = k == REC_RINS;
+      u32 ok = (h.w0 == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
+               (pr.w0 == (REC_RPARENT << 28)) & (pr.w1 == agent) & (pr.w2 == seq - 1u) & (ins | (k == REC_RDEL));
+      if (!ok || !fast_txn_ok(agent, seq, first)) return 0;
+      if (id_to_order(o.w1 & 0xFFFFu, o.w2, ol) != ST_OK || ol == ROOT_ORDER) return 0;  // origin_left / target
+      if (ins && id_to_order(o.w1 >> 16, o.w3, orr) != ST_OK) return 0;
+      if (!find_order(ol, true, c)) return 0;  // doc.rs:101-136 (loads the item's leaf)
+      c.off += ins;                             // get_cursor_after
     } else {
       agent = h.w1;
-      u32 lp = o.w1, del = o.w2, ins = o.w3;
-      l = del + ins;
+      u32 lp = o.w1, del = o.w2;
+      ins = o.w3 != 0u;
+      l = del + o.w3;
       u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l) &
-               ((del == 0u) != (ins == 0u)) & (l - 1u < 0xFFFFu) & (g(C_VS_OK) != 0u) & ((ins == 0u) | (lp != 0u));
+               ((del != 0u) != ins) & (l - 1u < 0xFFFFu) & ((lp != 0u) | !ins);
       if (!ok || !fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first)) return 0;
-      u32 at = ins ? lp - 1u : lp;  // insert: origin_left is the item at pos - 1 (doc.rs:446-447)
-      u32 vs = g(C_VSTART);
-      if ((at < vs) | (at - vs >= g(C_NOW))) return 0;  // outside the cached leaf's visible range
-      if (!w.cfind_content(g(C_N), at - vs, idx, off)) return 0;
-      i32 el = w.cget_len(idx);
-      if (ins) {
-        if (off + 1u != (u32)el) return 0;  // origin_left ends its entry
-        u32 nxo, has = next_item_after(idx, nxo);
-        return fast_typing(b0, nv, 0u, idx, has ? nxo : ROOT_ORDER, agent, o, first);
-      }
-      if (off + l > (u32)el) return 0;
+      if (!cursor_at_content_pos(ins ? lp - 1u : lp, c)) return 0;  // root.rs:54-88 (loads the leaf)
+      ol = w.cget_order(c.idx) + c.off;  // doc.rs:446-449: the item at pos - 1, then Cursor::next
+      c.off += ins;
     }
-    return fast_deletes(b0, nv, remote, agent, idx, off, l, first, o);
+    u32 idx = c.idx;
+    if (ins) {
+      u32 el = slen_i(w.cget_len(idx)), nxo, has;
+      if (c.off < el) { nxo = w.cget_order(idx) + c.off; has = 1; }
+      else has = next_item_after(idx, nxo);
+      if (remote) {
+        if (has && nxo != orr) return 0;  // integrate would scan (doc.rs:183-221)
+      } else {
+        orr = has ? nxo : ROOT_ORDER;  // doc.rs:453; integrate then stops at once
+      }
+      Span item{first, ol, orr, (i32)l};
+      Span e = w.cget(idx);
+      if ((c.off == el) & can_append(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
+      if (!leaf_insert(idx, c.off, item)) return 0;
+      fast_txn_commit(first, l);
+      return per;
+    }
+    i32 el = w.cget_len(idx);
+    if ((el <= 0) | (c.off + l > (u32)el)) return 0;  // already deleted / spans entries
+    return fast_deletes(b0, nv, remote, agent, idx, c.off, l, first, o);
   }
 
   // Replay this document's record stream from its rec_pos.  A GEN record stays current until
