@@ -1077,13 +1077,26 @@ struct Replayer {
     if (!((e.len > 0) & (e.order + (u32)e.len == first) & (e.orr == orr))) return 0;
     u32 total;
     u32 nt = w.typing_scan(b0, nv, remote, agent, o.w1, o.w3, total);
+    // The run may go on past the window: slide the window to its last txn and scan on.
+    u32 per = remote ? 3u : 2u, rn = rec_n();
+    u32 pos0 = g(T_RB_BASE) + b0;
+    while ((pos0 + (nt + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
+      u32 last = pos0 + (nt - 1u) * per;
+      rec_window(last);
+      nv = rn - last < 64u ? rn - last : 64u;
+      u32 t2;
+      u32 n2 = w.typing_scan(0u, nv, remote, agent, o.w1, o.w3, t2);
+      if (n2 <= 1u) break;
+      total += t2 - w.rec_get(0u).w3;
+      nt += n2 - 1u;
+    }
     if (g(K_MAP) - first < total) return 0;     // capacity: the general path stops exactly
     w.fill(lof() + first, total, g(C_LEAF));   // notify (doc.rs:143-153)
     e.len += (i32)total;
     set(idx, e);
     inc(S_N_ITEMS, total);
     fast_txn_commit(first, total);
-    return nt * (remote ? 3u : 2u);
+    return nt * per;
   }
   // Delete `l` items at offset `off` of visible entry idx of the cached leaf: mutate_entry
   // (mutations.rs:227-277) and insert_internal's prepend / shift (mutations.rs:84-146) without a
@@ -1140,11 +1153,22 @@ struct Replayer {
       back = delta == 0xFFFFFFFFu;
       u32 fwd = delta == (remote ? 1u : 0u);
       if (back | fwd) {
-        k = w.delete_scan(b0, nv, remote, agent, delta);
         u32 room = back ? off + 1u : (u32)w.cget_len(idx) - off;  // targets stay in this entry
         if (remote) {  // ... and in the author's last item_orders run (contiguous orders)
           u32 r2 = back ? o.w2 - key + 1u : key + g(T_AGL_LEN) - o.w2;
           room = room < r2 ? room : r2;
+        }
+        k = w.delete_scan(b0, nv, remote, agent, delta);
+        // the run may go on past the window: slide the window to its last txn and scan on
+        u32 rn = rec_n();
+        u32 pos0 = g(T_RB_BASE) + b0;
+        while ((k < room) & (pos0 + (k + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
+          u32 last = pos0 + (k - 1u) * per;
+          rec_window(last);
+          nv = rn - last < 64u ? rn - last : 64u;
+          u32 n2 = w.delete_scan(0u, nv, remote, agent, delta);
+          if (n2 <= 1u) break;
+          k += n2 - 1u;
         }
         k = k < room ? k : room;
       }
