@@ -119,12 +119,12 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
 
 template <int L>
 __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
-  u32 d = blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
   if (d >= n) return;
   ROOT_LDS;
   WaveGPU<L> w = wave_with_root<L>(s_root);
   DocState s = w.ldT(P.st + d);
-  DocSeg seg = P.seg[d];
+  DocSeg seg = w.ld_seg(P.seg + d);
   u32 l = lane_id();
   if (s.status != ST_OK && s.status != ST_NEED_CAPACITY) {
     if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
@@ -132,33 +132,57 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   }
   Span* canon = O.canon + seg.leaf_base * L;
   u32* vpos = O.vpos + seg.leaf_base * L;
+  const Span* leaves = P.leaves + seg.leaf_base * L;
   w.root_load(P.groups + seg.grp_base, s.ng);
-  u32 out = 0, vis = 0;
-  bool have = false;
+  // Canonical spans, one leaf per step, lane i = entry i: an entry starts a new span unless
+  // YjsSpan::can_append(previous entry, entry) (span.rs:47-53; merging is transitive, so the
+  // previous raw entry stands for the open span); span lengths are segmented sums of a prefix
+  // scan; the span still open at the leaf's end carries over (uniform registers).
+  u32 out = 0, vis = 0, have = 0;
   Span open{0, 0, 0, 0};
   u32 open_vpos = 0;
   for (u32 g = 0; g < s.ng; g++) {
     u32 blk = w.root_blk(g), cnt = w.root_cnt(g);
-    const u32* dl = P.dir_leaf + (seg.blk_base + blk) * GROUP;
-    u32 mydl = l < cnt ? dl[l] : 0u;
+    u32 mydl = P.dir_leaf[(seg.blk_base + blk) * GROUP + l];  // 64-slot row: always in bounds
     for (u32 i = 0; i < cnt; i++) {
       u32 leaf = rdlane(mydl, i);
-      u32 nn = w.cache_load(P.leaves + (seg.leaf_base + leaf) * L);
-      for (u32 j = 0; j < nn; j++) {
-        Span sp = w.cget(j);
-        if (have && can_append(open, sp)) {
-          open.len += sp.len;
-        } else {
-          if (have) {
-            if (l == 0) { canon[out] = open; vpos[out] = open_vpos; }
-            out++;
-          }
-          open = sp;
-          open_vpos = vis;
-          have = true;
+      uint4 v = *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1)));
+      bool valid = l < (u32)L && v.w != 0u;  // entries are packed at the front of a leaf
+      u32 nn = (u32)__popcll(ballot(valid));
+      Span e{v.x, v.y, v.z, (i32)v.w};
+      u32 px = shfl(v.x, l - 1u), py = shfl(v.y, l - 1u), pz = shfl(v.z, l - 1u), pw = shfl(v.w, l - 1u);
+      Span prev = l == 0u ? open : Span{px, py, pz, (i32)pw};
+      bool app = valid && (l != 0u || have) && can_append(prev, e);
+      bool start = valid && !app;
+      u64 M = ballot(start);
+      u32 len_u = valid ? v.w : 0u;
+      u32 Pl = wave_incl_scan(len_u);  // signed lengths, two's complement sums
+      u32 cl = valid && (i32)v.w > 0 ? v.w : 0u;
+      u32 V = wave_incl_scan(cl);
+      u32 leaf_vis = rdlane(V, 63);
+      u64 above = M & ~((2ull << l) - 1ull);
+      u32 nxt = above ? (u32)__builtin_ctzll(above) : nn;
+      u32 p_end = shfl(Pl, nxt - 1u);
+      i32 glen = (i32)(p_end - (Pl - len_u));  // span starting at this lane: lanes [l, nxt)
+      u32 fs = M ? (u32)__builtin_ctzll(M) : nn;
+      if (have && fs) open.len += (i32)rdlane(Pl, fs - 1u);
+      if (M) {
+        if (have) {
+          if (l == 0u) { canon[out] = open; vpos[out] = open_vpos; }
+          out++;
         }
-        vis += clen(sp);
+        u32 ls = 63u - (u32)__builtin_clzll(M);
+        u32 rank = (u32)__popcll(M & ((1ull << l) - 1ull));
+        if (start && l != ls) {
+          canon[out + rank] = Span{v.x, v.y, v.z, glen};
+          vpos[out + rank] = vis + V - cl;
+        }
+        out += (u32)__popcll(M) - 1u;
+        open = Span{rdlane(v.x, ls), rdlane(v.y, ls), rdlane(v.z, ls), (i32)rdlane((u32)glen, ls)};
+        open_vpos = vis + rdlane(V - cl, ls);
+        have = 1;
       }
+      vis += leaf_vis;
     }
   }
   if (have) {
@@ -170,12 +194,24 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   u32* so = O.span_of + seg.map_base;
   w.fill(so, s.next_order, INVALID);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  // 64 spans at a time: item j of the chunk finds its span by a 6-step search over the
+  // chunk's length prefix (lane-parallel, no per-lane serial loop over a span's items)
   u64 h = 0;
-  for (u32 k = l; k < out; k += 64) {
-    Span sp = canon[k];
-    u32 ln = slen(sp);
-    for (u32 t = 0; t < ln; t++) so[sp.order + t] = k;
-    h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
+  for (u32 k0 = 0; k0 < out; k0 += 64) {
+    u32 k = k0 + l;
+    Span sp = k < out ? canon[k] : Span{0, 0, 0, 0};
+    u32 ln = k < out ? slen(sp) : 0u;
+    if (k < out) h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
+    u32 Pi = wave_incl_scan(ln);
+    u32 T = rdlane(Pi, 63);
+    for (u32 t = 0; t < T; t += 64) {
+      u32 j = t + l;
+      u32 m = 0;
+      for (u32 step = 32; step; step >>= 1)
+        if (shfl(Pi, m + step - 1u) <= j) m += step;  // m = lanes whose prefix ends at or before j
+      u32 pm = shfl(Pi, m), lm = shfl(ln, m), om = shfl(sp.order, m);
+      if (j < T) so[om + (j - (pm - lm))] = k0 + m;
+    }
   }
   const CwoRun* cwo = P.cwo + seg.cwo_base;
   for (u32 k = l; k < s.n_cwo; k += 64) {
