@@ -149,8 +149,8 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
                 uint32_t* cwo4, uint32_t* del3, uint32_t* dd3, uint32_t* txn5, uint32_t* parents,
                 uint32_t* frontier);
 
-/* Raw per-document replay state (20 u32: status, resume point, table sizes, ...; debugging). */
-int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out20);
+/* Raw per-document replay state (22 u32: status, resume point, table sizes, ...; debugging). */
+int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out22);
 /* Device time of the last replay / publish launches in ms (HIP events on the engine stream). */
 int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms);
 /* Engine stream (hipStream_t) for callers that time or order their own work. */

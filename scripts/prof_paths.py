@@ -18,7 +18,7 @@ e.reset_async()
 e.run_async()
 e.sync()
 ms = e.timings()[0]
-s = np.array([e.debug_state(d) for d in range(0, n, max(1, n // 64))])
-fast, gen = s[:, 18].astype(np.float64), s[:, 19].astype(np.float64)
-print(f"docs {n} replay_ms {ms:.1f}  per-doc cycles: fast {fast.mean():.4g} generic {gen.mean():.4g} "
-      f"(generic share {gen.mean() / (fast.mean() + gen.mean()):.3f})")
+s = np.array([e.debug_state(d) for d in range(0, n, max(1, n // 64))]).astype(np.float64)
+c = {"typing": s[:, 18].mean(), "generic": s[:, 19].mean(), "delete": s[:, 20].mean(), "insert": s[:, 21].mean()}
+tot = sum(c.values())
+print(f"docs {n} replay_ms {ms:.1f}  per-doc clock ticks: " + "  ".join(f"{k} {v:.4g} ({v / tot:.1%})" for k, v in c.items()))

@@ -227,7 +227,7 @@ class Engine:
         return st[np.asarray(docs, dtype=np.int64)]
 
     def debug_state(self, doc: int) -> np.ndarray:
-        out = np.zeros(20, np.uint32)
+        out = np.zeros(22, np.uint32)
         _check(self.L.crdt_debug_state(self.h, doc, _p(out)), "debug_state")
         return out
 

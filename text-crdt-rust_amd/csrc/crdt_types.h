@@ -147,8 +147,8 @@ struct DocState {
   u32 ng, next_order, len, n_cwo;
   u32 n_del, n_dd, n_txn, n_par;
   u32 n_fr, n_agents, n_items, cap_need;
-  u32 n_entries, gen_done, prof0, prof1;  // gen_done: ops of the current GEN record applied;
-                                          // prof*: diagnostic cycle counters (-DCRDT_PROF)
+  u32 n_entries, gen_done;  // gen_done: ops of the current GEN record applied
+  u32 prof0, prof1, prof2, prof3;  // diagnostic cycle counters (-DCRDT_PROF builds only)
 };
 
 struct Pools {

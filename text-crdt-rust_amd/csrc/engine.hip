@@ -850,11 +850,11 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
   return 0;
 }
 
-int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out20) {
-  if (!valid(e) || doc >= e->n_docs || !out20) return CRDT_E_ARG;
+int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out22) {
+  if (!valid(e) || doc >= e->n_docs || !out22) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
-  HIPCHK(hipMemcpyAsync(out20, e->st + doc, sizeof(DocState), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(out22, e->st + doc, sizeof(DocState), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return 0;
 }

@@ -55,7 +55,7 @@ enum : u32 {
   S_BASE = 40,
   S_STATUS = 40, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
   S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES, S_GEN_DONE,
-  S_PROF0, S_PROF1,  // diagnostic builds (-DCRDT_PROF): cycles in fast paths / general interpreter
+  S_PROF0, S_PROF1, S_PROF2, S_PROF3,  // -DCRDT_PROF: cycles in typing / general / delete / insert paths
   // leaf cache bookkeeping
   C_LEAF = 64, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
@@ -69,12 +69,16 @@ enum : u32 {
   T_RB_BASE,
   N_SLOTS
 };
-static_assert(S_PROF1 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
+static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
+static_assert(S_PROF3 < 64, "DocState lives in the first context register");
 static_assert(N_SLOTS <= 128, "two context registers");
 
 template <class W, int L>
 struct Replayer {
   W w;  // owned by value: its lane registers stay SSA values, never a scratch object
+#ifdef CRDT_PROF
+  u32 prof_cat = 0;  // diagnostic: which fast path ran (0 typing, 2 delete, 3 insert)
+#endif
 
   // ------------------------------------------------------------------ context access
   CRDT_HD u32 g(u32 f) const { return w.xg(f); }
@@ -1135,6 +1139,65 @@ struct Replayer {
     }
     return 1;
   }
+  // A run of k >= 2 one-item deletes in closed form (the per-op rules of leaf_delete, solved once):
+  //  * backspacing from the last item of entry E (idx): every delete splits E's last item off and
+  //    either prepends it onto the entry after E or inserts it there.  A fresh single deleted item
+  //    {t, t-1} accepts the next one (YjsSpan::can_append), after which its origin_left equals
+  //    its order (span.rs:61-64) and it accepts no more: new entries alternate insert / prepend,
+  //    starting with a prepend onto the next entry N0 iff can_append(first deleted item, N0);
+  //  * forward deleting from item `off` of E (the remainder never prepends onto the next
+  //    entry): E becomes [E[..off]] [k single deleted items] [the rest of E].
+  // Returns k' <= k deletes applied (0: not this shape / no room; nothing changed).
+  CRDT_HD u32 delete_run_closed(u32 idx, u32 off, u32 t1, u32 k, u32 back) {
+    Span E = w.cget(idx);
+    u32 n = g(C_N);
+    u32 orr = E.orr;
+    u32 has_nx = idx + 1u < n;
+    Span N0 = w.cget(idx + 1u);
+    u32 room = (u32)L - n;  // new entries the leaf can take
+    u32 delta;
+    if (back) {
+      if (off + 1u != (u32)E.len) return 0;  // not from the entry's last item
+      u32 p0 = has_nx && can_append(Span{t1, t1 - 1u, orr, -1}, N0);
+      u32 kmax = 2u * room + p0;
+      k = k < off ? k : off;  // E keeps its first item (deleting it is a different shape)
+      k = k < kmax ? k : kmax;
+      if (k < 2u) return 0;
+      delta = p0 ? k / 2u : (k + 1u) / 2u;  // new entries F_1..F_delta, newest first after E
+      w.cache_shift_right(idx + 1u, n, delta);
+      w.cset_lanes(idx + 1u, idx + 1u + delta, [&](u32 lane) {
+        u32 q = delta - (lane - idx - 1u);           // F_q
+        u32 jc = p0 ? 2u * q : 2u * q - 1u;          // the op (1-based) that created it
+        u32 tc = t1 - (jc - 1u);
+        return jc + 1u <= k ? Span{tc - 1u, tc - 1u, orr, -2} : Span{tc, tc - 1u, orr, -1};
+      });
+      if (p0) w.cset(idx + 1u + delta, Span{t1, N0.ol, N0.orr, N0.len - 1});
+      E.len = (i32)(off + 1u - k);
+      w.cset(idx, E);
+    } else {
+      u32 ha = off > 0u;
+      if (has_nx && can_append(Span{t1 + 1u, t1, orr, E.len - (i32)off - 1}, N0)) return 0;
+      u32 kmax = room > ha ? room - ha : 0u;  // adds ha + k entries with a remainder (one fewer without)
+      k = k < kmax ? k : kmax;
+      if (k < 2u) return 0;
+      u32 rest = (u32)E.len - off - k;
+      u32 cnt = ha + k + (rest != 0u);
+      delta = cnt - 1u;
+      w.cache_shift_right(idx + 1u, n, delta);
+      w.cset_lanes(idx, idx + cnt, [&](u32 lane) {
+        u32 p = lane - idx;
+        u32 j = p - ha;  // deleted item j (0-based), or the remainder when j == k
+        if (ha && p == 0u) return Span{E.order, E.ol, orr, (i32)off};
+        if (j < k) return Span{t1 + j, (j == 0u && !ha) ? E.ol : t1 + j - 1u, orr, -1};
+        return Span{t1 + k, t1 + k - 1u, orr, (i32)rest};
+      });
+    }
+    p(C_N, n + delta);
+    inc(S_N_ENTRIES, delta);
+    p(C_NOW, g(C_NOW) - k);
+    p(C_DIRTY, 1u);
+    return k;
+  }
   // Delete txns: the one at b0 (l items at `off` of entry idx) and, when it deletes one item, the
   // run of one-item delete txns that follows it in the prefetch block -- backspacing (each
   // deletes the item before the previous one) or forward deleting (the item after) -- validated
@@ -1174,14 +1237,16 @@ struct Replayer {
       }
     }
     if ((g(K_MAP) - first < k * l) | (g(K_DEL) - g(S_N_DEL) < k)) return 0;
-    u32 done = 0;
-    for (u32 j = 0; j < k; j++) {
-      u32 ij = back ? idx : (j == 0u ? idx : idx + (off > 0u) + j);  // forward: the remainder moves right
-      u32 oj = back ? off - j : (j == 0u ? off : 0u);
-      u32 tj = back ? t1 - j : t1 + j;
-      if ((w.cget_order(ij) + oj != tj) | (w.cget_len(ij) <= (i32)oj)) break;
-      if (!leaf_delete(ij, oj, l)) break;
-      done++;
+    u32 done = k >= 2u ? delete_run_closed(idx, off, t1, k, back) : 0u;
+    if (done == 0u) {  // op by op
+      for (u32 j = 0; j < k; j++) {
+        u32 ij = back ? idx : (j == 0u ? idx : idx + (off > 0u) + j);  // forward: the remainder moves right
+        u32 oj = back ? off - j : (j == 0u ? off : 0u);
+        u32 tj = back ? t1 - j : t1 + j;
+        if ((w.cget_order(ij) + oj != tj) | (w.cget_len(ij) <= (i32)oj)) break;
+        if (!leaf_delete(ij, oj, l)) break;
+        done++;
+      }
     }
     if (done == 0u) return 0;
     if (back) {  // doc.rs:305-308 / 420-423: backspaced targets never coalesce: one run each
@@ -1283,6 +1348,9 @@ struct Replayer {
       }
       Span item{first, ol, orr, (i32)l};
       Span e = w.cget(idx);
+#ifdef CRDT_PROF
+      prof_cat = ((c.off == el) & can_append(e, item)) ? 0u : 3u;
+#endif
       if ((c.off == el) & can_append(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
       if (!leaf_insert(idx, c.off, item)) return 0;
       fast_txn_commit(first, l);
@@ -1290,6 +1358,9 @@ struct Replayer {
     }
     i32 el = w.cget_len(idx);
     if ((el <= 0) | (c.off + l > (u32)el)) return 0;  // already deleted / spans entries
+#ifdef CRDT_PROF
+    prof_cat = 2u;
+#endif
     return fast_deletes(b0, nv, remote, agent, idx, c.off, l, first, o);
   }
 
@@ -1319,8 +1390,11 @@ struct Replayer {
         u32 fast = gen ? 0u : fast_txn(pos, kind);
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
-        if (fast) inc(S_PROF0, (u32)(t1 - t0));
-        else inc(S_PROF1, (u32)(t1 - t0));
+        u32 dt = (u32)(t1 - t0);
+        if (!fast) inc(S_PROF1, dt);
+        else if (prof_cat == 0u) inc(S_PROF0, dt);
+        else if (prof_cat == 2u) inc(S_PROF2, dt);
+        else inc(S_PROF3, dt);
 #endif
         if (fast) { pos += fast; continue; }
         bool remote = kind == REC_RTXN;

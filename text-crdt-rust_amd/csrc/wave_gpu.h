@@ -183,6 +183,16 @@ struct WaveGPU {
     er = me ? s.orr : er;
     en = me ? s.len : en;
   }
+  // entries [a, b) := f(lane), lane-parallel (f computes each lane's entry in VALU)
+  template <class F> __device__ __forceinline__ void cset_lanes(u32 a, u32 b, F f) {
+    u32 l = lane_id();
+    Span s = f(l);
+    bool in = l >= a && l < b;
+    eo = in ? s.order : eo;
+    el = in ? s.ol : el;
+    er = in ? s.orr : er;
+    en = in ? s.len : en;
+  }
   // lanes [a, b) as a mask, and the lowest lane of a mask (wave-uniform)
   __device__ __forceinline__ u64 lanes_in(u32 a, u32 b) const { u32 l = lane_id(); return ballot(l >= a && l < b); }
   __device__ __forceinline__ static u32 first_lane(u64 m) { return (u32)__builtin_ctzll(m); }
