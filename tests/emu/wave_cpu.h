@@ -103,11 +103,17 @@ struct WaveCPU {
     for (u32 i = 0; i < n; i++) if (order >= c[i].order && order - c[i].order < slen(c[i])) return (i32)i;
     return -1;
   }
-  void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) const {
-    for (u32 j = 0; j < (u32)L; j++) {
+  Span mv[64];
+  void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) {
+    for (u32 j = 0; j < 64; j++) {
       u32 src = j + idx - padding;
-      dst[j] = (j >= padding && src < n) ? c[src] : Span{0, 0, 0, 0};
+      mv[j] = (j < (u32)L && j >= padding && src < n) ? c[src] : Span{0, 0, 0, 0};
+      if (j < (u32)L) dst[j] = mv[j];
     }
+  }
+  void cache_from_moved() { for (u32 j = 0; j < 64; j++) c[j] = mv[j]; }
+  void fill_runs(u32* base, u32 a, u32 b, u32 v) const {
+    for (u32 i = a; i < b; i++) for (u32 t = 0; t < slen(c[i]); t++) base[c[i].order + t] = v;
   }
   void cache_clear(u32 a, u32 b) { for (u32 i = a; i < b; i++) c[i] = Span{0, 0, 0, 0}; }
   void cache_shift_right(u32 idx, u32 n, u32 k) {

@@ -469,10 +469,7 @@ struct Replayer {
     u32 stolen = w.cache_vis_from(idx);
     u32 first_moved = w.cget_order(idx);
     w.cache_write_moved(leafp(nl), idx, n, padding);
-    for (u64 m = w.lanes_in(idx, n); m; m &= m - 1) {  // notify every moved entry
-      Span e = w.cget(w.first_lane(m));
-      w.fill(lof() + e.order, slen(e), nl);
-    }
+    w.fill_runs(lof(), idx, n, nl);  // notify every moved entry
     w.cache_clear(idx, n);
     p(C_NOW, g(C_NOW) - stolen);
     p(C_N, idx);
@@ -559,10 +556,17 @@ struct Replayer {
     if (cn + space > (u32)L) {
       bool follow = c.idx >= (u32)L / 2;
       u32 moved = cn - c.idx;
+      u32 succ = g(C_SUCC), succ_ord = g(C_SUCC_ORD);  // the old leaf's successor follows nl
       u32 nl = split_at(c.idx, follow ? space : 0u);
       if (follow) {  // the cursor follows the new leaf; its first `space` slots are padding
+        u32 nblk = g(C_BLK), ni = g(C_I) + 1u;  // nl sits right after the old leaf
         commit();
-        ensure(nl);
+        // nl becomes the cached leaf straight from registers (split_at just wrote it to HBM)
+        w.cache_from_moved();
+        u32 v = w.cache_vis_from(0u);
+        p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 0); p(C_VS_OK, 0);
+        p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
         p(C_N, space + moved);
         c.leaf = nl;
         c.idx = 0;

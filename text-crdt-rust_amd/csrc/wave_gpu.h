@@ -235,12 +235,33 @@ struct WaveGPU {
     u64 m = ballot(l < n && order >= eo && order - eo < sl);
     return m ? (i32)(__builtin_ctzll(m)) : -1;
   }
-  __device__ __forceinline__ void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) const {
+  // the split-off entries [idx, n) of the cached leaf, after `padding` empty slots: written to
+  // the new leaf and kept in registers (cache_from_moved) for a cursor that follows them
+  u32 mo = 0, ml = 0, mr = 0, mn = 0;
+  __device__ __forceinline__ void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) {
     u32 l = lane_id();
     u32 src = l + idx - padding;  // valid only when l >= padding
     u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
-    bool take = l >= padding && src < n;
-    if (l < (u32)L) *(uint4*)(dst + l) = take ? make_uint4(o, a, b, c) : make_uint4(0, 0, 0, 0);
+    bool take = l >= padding && src < n && l < (u32)L;
+    mo = take ? o : 0u; ml = take ? a : 0u; mr = take ? b : 0u; mn = take ? c : 0u;
+    if (l < (u32)L) *(uint4*)(dst + l) = make_uint4(mo, ml, mr, mn);
+  }
+  __device__ __forceinline__ void cache_from_moved() { eo = mo; el = ml; er = mr; en = (i32)mn; }
+  // lof[order + t] = v for every item of the entries in lanes [a, b): 64 items per step, each
+  // lane finding its entry by a 6-step search over the entries' length prefix
+  __device__ __forceinline__ void fill_runs(u32* base, u32 a, u32 b, u32 v) const {
+    u32 l = lane_id();
+    u32 ln = l >= a && l < b ? (u32)(en < 0 ? -en : en) : 0u;
+    u32 Pi = wave_incl_scan(ln);
+    u32 T = rdlane(Pi, 63);
+    for (u32 t = 0; t < T; t += 64) {
+      u32 j = t + l;
+      u32 m = 0;
+      for (u32 step = 32; step; step >>= 1)
+        if (shfl(Pi, m + step - 1u) <= j) m += step;
+      u32 pm = shfl(Pi, m), lm = shfl(ln, m), om = shfl(eo, m);
+      if (j < T) base[om + (j - (pm - lm))] = v;
+    }
   }
   __device__ __forceinline__ void cache_clear(u32 a, u32 b) {
     u32 l = lane_id();
