@@ -105,6 +105,7 @@ struct EmuDoc {
     if (need & 4u) { seg.del_cap = seg.del_cap * 2 + 16; dels.resize(seg.del_cap); }
     if (need & 8u) { seg.par_cap = seg.par_cap * 2 + 16; parents.resize(seg.par_cap); }
     if (need & 16u) { seg.map_cap = seg.map_cap * 2 + 16; leaf_of.resize(seg.map_cap, 0xDEADBEEFu); }
+    if (need & 64u) { seg.dd_cap = seg.dd_cap * 2 + 64; dd.resize(seg.dd_cap); }
     if (need & 32u) {  // re-space every agent's run list with doubled capacity
       std::vector<ARun> na;
       for (u32 a = 0; a < st.n_agents; a++) {

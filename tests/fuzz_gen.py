@@ -159,3 +159,46 @@ def concurrent_wire(seed: int, n_agents: int = 3, rounds: int = 6, ops_per_round
                 return build_wire(history), len(history)
             seen[i] = len(history)
     return build_wire(history), len(history)
+
+
+def config5_wire(seed: int, base_len: int = 4096, n_agents: int = 16, rounds: int = 8, ops: int = 4,
+                 hot: int = 32, del_frac: float = 0.6):
+    """BASELINE config 5 shape: concurrent, deletion-heavy.
+
+    Agent "base" inserts `base_len` chars (one txn, contiguous orders).  Then `rounds` rounds: each
+    of `n_agents` agents makes `ops` single-op txns against the round-start snapshot -- 60 %
+    deletes of 1..64 base items (contiguous targets, Q4; overlapping deletes make double deletes),
+    40 % inserts of 1..8 chars at one of `hot` shared hotspots (origin_left = base item h,
+    origin_right = base item h+1, so concurrent inserts tie in integrate's Equal branch).  A txn's
+    parents are the round-start frontier (first txn of the agent in the round) or the agent's
+    previous txn.  Delivery within a round is a seeded interleaving that keeps each agent's order.
+    Returns the wire batch (one causally ordered history)."""
+    rng = random.Random(seed)
+    names = [f"a{i:02d}_{rng.randrange(1 << 20):05x}" for i in range(n_agents)]
+    R = ("ROOT", 0xFFFFFFFF)
+    txns = [("base", 0, [R], [(0, "ROOT", R[1], "ROOT", R[1], base_len)])]
+    hotspots = sorted(rng.sample(range(base_len - 1), min(hot, base_len - 1)))
+    frontier = [("base", base_len - 1)]
+    seq = {a: 0 for a in names}
+    for _ in range(rounds):
+        per_agent = {}
+        for a in names:
+            lst, parents = [], list(frontier)
+            for _ in range(ops):
+                if rng.random() < del_frac:
+                    ln = rng.randint(1, min(64, base_len))
+                    s = rng.randrange(0, base_len - ln + 1)
+                    op = (1, "base", s, None, 0, ln)
+                else:
+                    h = rng.choice(hotspots)
+                    ln = rng.randint(1, 8)
+                    op = (0, "base", h, "base", h + 1, ln)
+                lst.append((a, seq[a], parents, [op]))
+                seq[a] += ln
+                parents = [(a, seq[a] - 1)]
+            per_agent[a] = lst
+        while any(per_agent.values()):
+            a = rng.choice([k for k, v in per_agent.items() if v])
+            txns.append(per_agent[a].pop(0))
+        frontier = [(a, seq[a] - 1) for a in names]
+    return build_wire(txns)

@@ -64,3 +64,18 @@ def test_generated_config4(seed):
         assert e.run_random(e.agent("gen"), n_ops, 0x9E3779B9 * (seed + 1), 400) == 0  # tight caps: growth
         assert e.check() == ""
         assert diff_states(o.export(), e.export()) == []
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_concurrent_config5(seed):
+    # BASELINE config 5 shape (16 agents, deletion-heavy, hotspot ties, double deletes)
+    from fuzz_gen import config5_wire
+    w = config5_wire(seed, base_len=3000, rounds=6, ops=4)
+    for L in (32, 4):
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        assert o.apply_remote_wire(w) == 0
+        assert o.sizes()["dd"] > 0
+        e = EmuDoc(L)
+        assert e.run_wire(w, 48) == 0
+        assert e.check() == ""
+        assert diff_states(o.export(), e.export()) == []

@@ -188,3 +188,22 @@ def test_generated_config4():
         if d < 3:
             assert_same(e.export(d), o.export())
             check_queries(e, d, o)
+
+
+def test_concurrent_config5():
+    # BASELINE config 5 shape at reduced scale: per document a 64k-char base by agent "base",
+    # then 16 agents x 12 rounds x 4 concurrent txns (60 % deletes of 1..64 base items ->
+    # double deletes, 40 % inserts at 32 shared hotspots -> integrate ties), seeded delivery.
+    from fuzz_gen import config5_wire
+    wires = [config5_wire(100 + s, base_len=65536, rounds=12, ops=4) for s in range(12)]
+    e = crdt_amd.Engine(len(wires), 32)
+    st = e.apply_remote_wire(list(range(len(wires))), wires)
+    assert (st == 0).all(), st
+    dg = e.digests()
+    for i, w in enumerate(wires):
+        o = OracleDoc()
+        assert o.apply_remote_wire(w) == 0
+        assert int(dg[i]) == o.digest(), i
+        if i < 2:
+            assert_same(e.export(i), o.export())
+            check_queries(e, i, o)

@@ -427,6 +427,7 @@ struct crdt_engine {
         if (need & 4u) c.del = c.del * 2 + 16;
         if (need & 8u) c.par = c.par * 2 + 16;
         if (need & 16u) c.map = c.map * 2 + 16;
+        if (need & 64u) c.dd = c.dd * 2 + 64;
         if (need & 32u) for (auto& x : docs[d].agent_cap) x = x * 2 + 1;
         if (need == 0) {  // cannot grow: make it a hard capacity error
           DocState s = st_h[d];

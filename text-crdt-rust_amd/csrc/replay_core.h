@@ -830,6 +830,10 @@ struct Replayer {
     if (g(K_DEL) - g(S_N_DEL) < n_dels) need |= 4u;
     if (g(K_PAR) - g(S_N_PAR) < (remote ? n_parents : g(S_N_FR))) need |= 8u;
     if (g(K_MAP) - g(S_NEXT_ORDER) < txn_len) need |= 16u;
+    // double deletes (remote only): one txn adds at most 3 entries per existing entry it overlaps
+    // plus 2 per increment_delete_range call (<= one per deleted item)
+    u32 ndd = g(S_N_DD);
+    if (remote && n_dels && (u64)g(K_DD) - ndd < 3ull * ndd + 2ull * txn_len + 2ull) need |= 64u;
     use_agent(agent);
     if (g(T_AG_CAP) == g(T_AG_CNT)) need |= 32u;
     p(S_CAP_NEED, need);
