@@ -98,6 +98,12 @@ int crdt_stage_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, cons
                      const crdt_local_txn* txns, const crdt_local_op* ops);
 int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs,
                            const uint8_t* const* wire, const uint64_t* wire_len);
+/* Shared local streams: stream k = txns[stream_txn_off[k] .. stream_txn_off[k+1]) (ops concatenated
+ * in txn order); document docs[i] replays stream stream_of_doc[i].  Each stream is encoded and
+ * uploaded once (device copies per document), e.g. a corpus of documents drawn from few traces. */
+int crdt_stage_local_shared(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* stream_of_doc,
+                            uint32_t n_streams, const uint64_t* stream_txn_off, const crdt_local_txn* txns,
+                            const crdt_local_op* ops);
 /* One wire batch replicated to docs [0, n_docs) of a fresh engine; name index `rename_idx` of the
  * batch's name table is replaced per document by names[d] (randomised client ids). */
 int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t wire_len,

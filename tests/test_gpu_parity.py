@@ -207,3 +207,24 @@ def test_concurrent_config5():
         if i < 2:
             assert_same(e.export(i), o.export())
             check_queries(e, i, o)
+
+
+def test_mixed_corpus_config3():
+    # BASELINE config 3 shape: doc d replays [AP, RC, SV][splitmix64(d) % 3] (local txns), from
+    # shared streams; every digest must equal the committed oracle golden digest of its trace.
+    import json
+    import os
+    from bench import splitmix64
+    names = ["automerge-paper", "rustcode", "sveltecomponent"]
+    traces = [load_trace(n) for n in names]
+    gold = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "oracle_golden.json")))
+    n = 48
+    which = [splitmix64(d) % 3 for d in range(n)]
+    e = crdt_amd.Engine(n, 32)
+    ag = e.agent_intern(list(range(n)), ["jeremy"] * n)
+    e.stage_local_shared(list(range(n)), which, int(ag[0]), traces)
+    st = e.run()
+    assert (st == 0).all(), st
+    dg = e.digests()
+    for d in range(n):
+        assert int(dg[d]) == int(gold[f"{names[which[d]]}/L32"]["digest"], 16), d

@@ -81,6 +81,7 @@ def lib():
     L.crdt_stage_remote_wire.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(u64)]
     L.crdt_stage_remote_replicated.argtypes = [vp, C.c_char_p, u64, u32, P(C.c_char_p)]
     L.crdt_stage_random.argtypes = [vp, u64, P(u32), C.c_char_p, u32, u64]
+    L.crdt_stage_local_shared.argtypes = [vp, u64, P(u32), P(u32), u32, P(u64), vp, vp]
     L.crdt_debug_state.argtypes = [vp, u32, P(u32)]
     L.crdt_reset_async.argtypes = [vp]
     L.crdt_run.argtypes = [vp, P(i32)]
@@ -111,6 +112,7 @@ EXPORTED_SYMBOLS = [
     "crdt_sync", "crdt_pos_to_loc", "crdt_loc_to_pos", "crdt_pos_to_loc_dev_async", "crdt_loc_to_pos_dev_async",
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
+    "crdt_stage_local_shared",
 ]
 
 
@@ -215,6 +217,18 @@ class Engine:
     def stage_remote_replicated(self, wire: bytes, rename_idx: int, names: Sequence[str]):
         arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
         _check(self.L.crdt_stage_remote_replicated(self.h, wire, len(wire), rename_idx, arr), "stage_replicated")
+
+    # --- shared local streams (config 3 corpora): doc i replays traces[stream_of_doc[i]] as `agent`
+    def stage_local_shared(self, docs: Sequence[int], stream_of_doc: Sequence[int], agent: int, traces) -> None:
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        so = np.ascontiguousarray(stream_of_doc, dtype=np.uint32)
+        txn_off = np.concatenate([[0], np.cumsum([t.counts.shape[0] for t in traces])]).astype(np.uint64)
+        tx = np.zeros((int(txn_off[-1]), 2), np.uint32)
+        tx[:, 0] = agent
+        tx[:, 1] = np.concatenate([t.counts for t in traces])
+        ops = np.ascontiguousarray(np.concatenate([np.asarray(t.patches, np.uint32).reshape(-1, 3) for t in traces]))
+        _check(self.L.crdt_stage_local_shared(self.h, d.shape[0], _p(d), _p(so), len(traces), _p(txn_off, C.c_uint64),
+                                              tx.ctypes.data, ops.ctypes.data), "stage_local_shared")
 
     # --- config 4: make_random_change (doc.rs:544-569) generated on the device
     def stage_random(self, docs: Sequence[int], agent: str, n_ops: int, seed: int):

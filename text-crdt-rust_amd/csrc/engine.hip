@@ -8,6 +8,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "crdt_gpu.h"
@@ -329,6 +330,7 @@ struct crdt_engine {
     u64 off = 0;
     const std::vector<Rec>* prev = nullptr;
     u64 prev_off = 0;
+    std::unordered_map<const std::vector<Rec>*, u64> uploaded;  // shared stream -> first device copy
     std::vector<Rec> hb;
     u64 hb_off = 0;
     auto flush = [&]() -> int {
@@ -343,11 +345,13 @@ struct crdt_engine {
       const std::vector<Rec>& sv = *streams[i];
       sg.rec_base = off;
       sg.rec_n = (u32)sv.size();
+      auto up = uploaded.find(&sv);
       if (!sv.empty()) {
-        if (&sv == prev) {
+        if (&sv == prev || up != uploaded.end()) {
           r = flush();
           if (r) return r;
-          HIPCHK(hipMemcpyAsync(recs + off, recs + prev_off, sv.size() * sizeof(Rec), hipMemcpyDeviceToDevice, stream));
+          u64 src = &sv == prev ? prev_off : up->second;
+          HIPCHK(hipMemcpyAsync(recs + off, recs + src, sv.size() * sizeof(Rec), hipMemcpyDeviceToDevice, stream));
         } else if (sv.size() > (1u << 20)) {  // large stream: straight from the caller's vector
           r = flush();
           if (r) return r;
@@ -358,6 +362,7 @@ struct crdt_engine {
           hb.insert(hb.end(), sv.begin(), sv.end());
         }
       }
+      if (up == uploaded.end()) uploaded.emplace(&sv, off);
       prev = &sv;
       prev_off = off;
       off += sv.size();
@@ -551,6 +556,31 @@ static int stage_local_impl(crdt_engine* e, uint64_t n_docs, const uint32_t* doc
 int crdt_stage_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
                      const crdt_local_txn* txns, const crdt_local_op* ops) {
   return stage_local_impl(e, n_docs, docs, txn_off, txns, ops);
+}
+
+int crdt_stage_local_shared(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* stream_of_doc,
+                            uint32_t n_streams, const uint64_t* stream_txn_off, const crdt_local_txn* txns,
+                            const crdt_local_op* ops) {
+  if (!valid(e) || !docs || !stream_of_doc || !stream_txn_off || !n_streams) return CRDT_E_ARG;
+  std::vector<std::vector<Rec>> enc(n_streams);
+  std::vector<StreamNeeds> snd(n_streams);
+  u64 op = 0;
+  for (u64 t = 0; t < stream_txn_off[0]; t++) op += txns[t].n_ops;
+  for (u32 k = 0; k < n_streams; k++)
+    for (u64 t = stream_txn_off[k]; t < stream_txn_off[k + 1]; t++) {
+      encode_local_txn(enc[k], snd[k], txns[t].agent, (const u32*)(ops + op), txns[t].n_ops);
+      op += txns[t].n_ops;
+    }
+  std::vector<u64> ids(n_docs);
+  std::vector<StreamNeeds> needs(n_docs);
+  std::vector<const std::vector<Rec>*> sp(n_docs);
+  for (uint64_t i = 0; i < n_docs; i++) {
+    if (docs[i] >= e->n_docs || stream_of_doc[i] >= n_streams) return CRDT_E_ARG;
+    ids[i] = docs[i];
+    sp[i] = &enc[stream_of_doc[i]];
+    needs[i] = snd[stream_of_doc[i]];
+  }
+  return e->stage(ids, sp, needs);
 }
 
 int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint8_t* const* wire,
