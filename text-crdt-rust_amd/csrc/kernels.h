@@ -27,7 +27,9 @@ struct PubOut {
 template <int L>
 __device__ __forceinline__ WaveGPU<L> wave_with_root(u32 (*s_root)[3 * MAX_GROUPS]) {
   WaveGPU<L> w;
-  w.rt = s_root[uni(threadIdx.x >> 6)];
+  // the LDS address space survives into the member: root accesses are ds_* (lgkmcnt only);
+  // a generic pointer would make them flat ops, whose waits also drain every pending store
+  w.rt = (typename WaveGPU<L>::lds_u32*)s_root[uni(threadIdx.x >> 6)];
   return w;
 }
 

@@ -71,7 +71,8 @@ struct WaveGPU {
   // This wave's slice of the kernel's LDS: blk[MAX_GROUPS], cnt[MAX_GROUPS], vis[MAX_GROUPS]
   // (structure of arrays: lane-parallel sweeps are bank-conflict free).  Kept out of VGPRs so
   // that no register is ever indexed by a run-time group number.
-  u32* rt = nullptr;
+  typedef __attribute__((address_space(3))) u32 lds_u32;  // ds_read/ds_write, never flat
+  lds_u32* rt = nullptr;
 
   // ---- scalar memory helpers (every lane touches the same address: uniform results, and a
   //      store is then visible to every lane's later loads by per-thread program order)
@@ -394,9 +395,9 @@ struct WaveGPU {
   }
 
   // ---------------------------------------------------------------- directory root (VGPRs)
-  __device__ __forceinline__ u32* rblk() const { return rt; }
-  __device__ __forceinline__ u32* rcnt() const { return rt + MAX_GROUPS; }
-  __device__ __forceinline__ u32* rvis() const { return rt + 2 * MAX_GROUPS; }
+  __device__ __forceinline__ lds_u32* rblk() const { return rt; }
+  __device__ __forceinline__ lds_u32* rcnt() const { return rt + MAX_GROUPS; }
+  __device__ __forceinline__ lds_u32* rvis() const { return rt + 2 * MAX_GROUPS; }
   __device__ __forceinline__ void root_init(u32 blk, u32 cnt, u32 vis) {
     rblk()[0] = blk;  // every lane stores the same value: no branch
     rcnt()[0] = cnt;
