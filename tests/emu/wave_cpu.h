@@ -26,6 +26,8 @@ struct WaveCPU {
 
   static u64 clock() { return 0; }
   u32 ld(const u32* p) const { return *p; }
+  u32 ld_raw(const u32* p) const { return *p; }
+  static u32 uni_(u32 x) { return x; }
   void st(u32* p, u32 v) const { *p = v; }
   void st(i32* p, i32 v) const { *p = v; }
   template <class T> T ldT(const T* p) const { return *p; }

@@ -298,12 +298,15 @@ struct Replayer {
     dir_set_cached_vis(g(C_NOW));
     p(C_DIRTY, 0);
   }
-  CRDT_HD void load_cache(u32 leaf, u32 blk, u32 i) {
+  // Cache `leaf`; `slot` = its directory slot (blk << 6 | i), possibly a load still in flight:
+  // the leaf's entries are requested before the slot is first used, so both arrive together.
+  CRDT_HD void load_cache(u32 leaf, u32 slot) {
     commit();
     p(C_N, w.cache_load(leafp(leaf)));
+    u32 sl = w.uni_(slot);
     p(C_LEAF, leaf);
-    p(C_BLK, blk);
-    p(C_I, i);
+    p(C_BLK, sl >> 6);
+    p(C_I, sl & 63u);
     p(C_DIRTY, 0);
     u32 v = w.cache_vis_from(0u);
     p(C_NOW, v);
@@ -325,8 +328,8 @@ struct Replayer {
   }
   CRDT_HD void ensure(u32 leaf) {
     if (leaf == g(C_LEAF)) return;
-    u32 v = w.ld(sol() + leaf);
-    load_cache(leaf, v >> 6, v & 63u);
+    commit();
+    load_cache(leaf, w.ld_raw(sol() + leaf));  // slot and entries: one round trip
   }
   // set entry idx of the cached leaf (tracks the cached visible count exactly)
   CRDT_HD void set(u32 idx, const Span& e) {
@@ -405,7 +408,7 @@ struct Replayer {
       commit();
       u32 lf, blk, i;
       if (!find_by_pos(pos, lf, vs, blk, i)) return false;
-      if (lf != g(C_LEAF)) load_cache(lf, blk, i);
+      if (lf != g(C_LEAF)) load_cache(lf, (blk << 6) | i);
       p(C_VSTART, vs);
       p(C_VS_OK, 1);
     }

@@ -77,6 +77,9 @@ struct WaveGPU {
   // ---- scalar memory helpers (every lane touches the same address: uniform results, and a
   //      store is then visible to every lane's later loads by per-thread program order)
   __device__ __forceinline__ u32 ld(const u32* p) const { return uni(*(const u32*)p); }
+  // a load whose wait is deferred to the first uni_() of its value (overlaps later loads)
+  __device__ __forceinline__ u32 ld_raw(const u32* p) const { return *(const u32*)p; }
+  __device__ __forceinline__ static u32 uni_(u32 x) { return uni(x); }
   __device__ __forceinline__ void st(u32* p, u32 v) const { *(u32*)p = v; }
   __device__ __forceinline__ void st(i32* p, i32 v) const { *(i32*)p = v; }
   template <class T> __device__ __forceinline__ T ldT(const T* p) const {
