@@ -1091,11 +1091,13 @@ struct Replayer {
     Span e = w.cget(idx);
     if (!((e.len > 0) & (e.order + (u32)e.len == first) & (e.orr == orr))) return 0;
     u32 total;
-    u32 nt = w.typing_scan(b0, nv, remote, agent, o.w1, o.w3, total);
+    u32 nt = 1u;
+    total = o.w3;  // (a generated op: nv == 0, no record window to scan)
+    if (nv) nt = w.typing_scan(b0, nv, remote, agent, o.w1, o.w3, total);
     // The run may go on past the window: slide the window to its last txn and scan on.
     u32 per = remote ? 3u : 2u, rn = rec_n();
     u32 pos0 = g(T_RB_BASE) + b0;
-    while ((pos0 + (nt + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
+    while ((nv != 0u) & (pos0 + (nt + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
       u32 last = pos0 + (nt - 1u) * per;
       rec_window(last);
       nv = rn - last < 64u ? rn - last : 64u;
@@ -1305,19 +1307,26 @@ struct Replayer {
     return 1;
   }
   // Returns the records consumed by a fast-path txn at `pos`, or 0 (use apply_txn).
-  CRDT_HD u32 fast_txn(u32 pos, u32 kind) {
+  // gen: a txn expanded from a GEN record (header gh, op go; no record window, no runs).
+  CRDT_HD u32 fast_txn(u32 pos, u32 kind, u32 gen, const Rec& gh, const Rec& go) {
     u32 remote = kind == REC_RTXN;
     u32 per = remote ? 3u : 2u;
     u32 rn = rec_n();
-    if ((rn - pos < per) | (g(C_LEAF) == INVALID)) return 0;
-    u32 b0 = pos - g(T_RB_BASE);
-    if (b0 + per > 64u) {  // move the window to the txn (and what follows it)
-      rec_window(pos);
-      b0 = 0;
+    if (g(C_LEAF) == INVALID) return 0;
+    u32 b0 = 0, nv = 0;
+    Rec h = gh, o = go;
+    if (!gen) {
+      if (rn - pos < per) return 0;
+      b0 = pos - g(T_RB_BASE);
+      if (b0 + per > 64u) {  // move the window to the txn (and what follows it)
+        rec_window(pos);
+        b0 = 0;
+      }
+      nv = rn - g(T_RB_BASE);
+      nv = nv < 64u ? nv : 64u;
+      h = w.rec_get(b0);
+      o = w.rec_get(b0 + 1u);
     }
-    u32 nv = rn - g(T_RB_BASE);
-    nv = nv < 64u ? nv : 64u;
-    Rec h = w.rec_get(b0), o = w.rec_get(b0 + 1u);
     u32 first = g(S_NEXT_ORDER);
     u32 agent, l, ins, ol = 0, orr = ROOT_ORDER;
     Cursor c;
@@ -1398,7 +1407,7 @@ struct Replayer {
 #ifdef CRDT_PROF
         u64 t0 = w.clock();
 #endif
-        u32 fast = gen ? 0u : fast_txn(pos, kind);
+        u32 fast = fast_txn(pos, kind, gen, h, gop);
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
         u32 dt = (u32)(t1 - t0);
@@ -1407,7 +1416,11 @@ struct Replayer {
         else if (prof_cat == 2u) inc(S_PROF2, dt);
         else inc(S_PROF3, dt);
 #endif
-        if (fast) { pos += fast; continue; }
+        if (fast) {
+          if (gen) inc(S_GEN_DONE);
+          else pos += fast;
+          continue;
+        }
         bool remote = kind == REC_RTXN;
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
         consumed = gen ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
