@@ -1,0 +1,117 @@
+"""GPU edge cases (SURVEY §4 test strategy): empty and ragged batches, very long ops, many agents,
+errors in the middle of a batch, documents that grow every table.  Each compares the HIP engine
+(through the C ABI) with the oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import crdt_amd  # noqa: E402
+from oracle_lib import OracleDoc  # noqa: E402
+from fuzz_gen import random_local_trace, concurrent_wire  # noqa: E402
+from test_gpu_parity import assert_same, check_queries  # noqa: E402
+
+
+def test_empty_and_ragged_batch():
+    # documents with 0, 1, 2, 17, 3000 and 20000 ops in one launch (ragged work per wave)
+    sizes = [0, 1, 2, 17, 3000, 20000]
+    e = crdt_amd.Engine(len(sizes), 32)
+    ag = e.agent_intern(list(range(len(sizes))), ["x"] * len(sizes))
+    per_doc, oracles = [], []
+    for i, n in enumerate(sizes):
+        o = OracleDoc()
+        a = o.agent("x")
+        if n:
+            c, p = random_local_trace(50 + i, n, ins_max=3)
+            off = np.concatenate([[0], np.cumsum(c)]).astype(int)
+            per_doc.append((i, [(int(ag[i]), p[off[k]:off[k + 1]]) for k in range(len(c))]))
+            assert o.apply_trace(a, c, p) == 0
+        oracles.append(o)
+    st = e.apply_local(per_doc)
+    assert (st == 0).all(), st
+    dg = e.digests()
+    for i, o in enumerate(oracles):
+        assert int(dg[i]) == o.digest(), i
+        assert int(e.lens()[i]) == len(o)
+        assert_same(e.export(i), o.export())
+    # a document that never saw an op answers queries like an empty ListCRDT
+    ag_, sq = e.pos_to_loc(np.zeros(3, np.uint32), np.arange(3, dtype=np.uint32))
+    assert (ag_ == 0xFFFF).all() and (sq == 0xFFFFFFFF).all()
+
+
+def test_long_ops_take_the_general_path():
+    # one 1,000,000-char insert, deletes of up to 70,000 chars, inserts of 65,536+ chars
+    ops = [[(0, 0, 1_000_000)], [(123_456, 70_000, 0)], [(5, 0, 65_536)], [(900_000, 1, 70_001)],
+           [(0, 500_000, 3)], [(10, 10, 10)]]
+    e = crdt_amd.Engine(1, 32)
+    a = int(e.agent_intern([0], ["big"])[0])
+    st = e.apply_local([(0, [(a, o) for o in ops])])
+    assert st[0] == 0
+    o = OracleDoc()
+    oa = o.agent("big")
+    for op in ops:
+        assert o.apply_local(oa, op) == 0
+    assert_same(e.export(0), o.export())
+    assert int(e.digests()[0]) == o.digest()
+
+
+def test_many_agents_concurrent():
+    # 40 concurrent agents: name ranks decide integrate ties (doc.rs:204-216)
+    wires = [concurrent_wire(700 + s, n_agents=40, rounds=3, ops_per_round=2)[0] for s in range(3)]
+    e = crdt_amd.Engine(len(wires), 32)
+    st = e.apply_remote_wire(list(range(len(wires))), wires)
+    for i, w in enumerate(wires):
+        o = OracleDoc()
+        so = o.apply_remote_wire(w)
+        assert st[i] == so
+        if so == 0:
+            assert_same(e.export(i), o.export())
+            check_queries(e, i, o)
+
+
+def test_error_mid_batch_poisons_only_its_document():
+    # doc 1's third txn deletes past the end (root.rs:160 panic in the reference): doc 1 stops
+    # with POS_OOB; docs 0 and 2 finish and match the oracle; doc 1 skips its later txns
+    good = [[(0, 0, 5)], [(2, 1, 0)], [(4, 0, 2)]]
+    bad = [[(0, 0, 5)], [(2, 1, 0)], [(3, 5, 0)], [(0, 0, 1)]]
+    e = crdt_amd.Engine(3, 32)
+    ag = e.agent_intern([0, 1, 2], ["p"] * 3)
+    st = e.apply_local([(0, [(int(ag[0]), o) for o in good]), (1, [(int(ag[1]), o) for o in bad]),
+                        (2, [(int(ag[2]), o) for o in good])])
+    assert list(st) == [0, -1, 0]
+    o = OracleDoc()
+    a = o.agent("p")
+    for op in good:
+        o.apply_local(a, op)
+    dg = e.digests()
+    assert int(dg[0]) == int(dg[2]) == o.digest()
+    # the poisoned document accepts no further ops
+    st2 = e.apply_local([(1, [(int(ag[1]), [(0, 0, 1)])])])
+    assert st2[0] == -1
+
+
+def test_tables_grow_during_replay():
+    # 200 agents interleaving local txns on one document: every RLE table (client_with_order,
+    # item_orders per agent, txns, deletes) outgrows its first capacity and resumes (ST_NEED_CAPACITY)
+    rng = np.random.default_rng(3)
+    e = crdt_amd.Engine(1, 32)
+    names = [f"agent{i:03d}" for i in range(200)]
+    ags = e.agent_intern([0] * len(names), names)
+    o = OracleDoc()
+    oags = [o.agent(n) for n in names]
+    txns, n = [], 0
+    for k in range(6000):
+        i = int(rng.integers(len(names)))
+        if n == 0 or rng.random() < 0.6:
+            op = (int(rng.integers(n + 1)), 0, int(rng.integers(1, 4)))
+            n += op[2]
+        else:
+            p = int(rng.integers(n))
+            op = (p, int(rng.integers(1, min(6, n - p) + 1)), 0)
+            n -= op[1]
+        txns.append((int(ags[i]), [op]))
+        assert o.apply_local(oags[i], [op]) == 0
+    st = e.apply_local([(0, txns)])
+    assert st[0] == 0
+    assert_same(e.export(0), o.export())
+    assert int(e.digests()[0]) == o.digest()
