@@ -1087,33 +1087,41 @@ struct Replayer {
   // origin_right = the item after that entry (or none).  integrate stops at once (doc.rs:184-190)
   // and insert_internal appends to the entry (mutations.rs:57-80, YjsSpan::can_append); every
   // later txn of the run is the same case.  Returns records consumed (0: not applicable).
-  CRDT_HD u32 fast_typing(u32 b0, u32 nv, u32 remote, u32 idx, u32 orr, u32 agent, const Rec& o, u32 first) {
-    Span e = w.cget(idx);
-    if (!((e.len > 0) & (e.order + (u32)e.len == first) & (e.orr == orr))) return 0;
-    u32 total;
+  // The run of typing txns starting with the one at b0 (validated by the caller): W::typing_scan
+  // over the window, continued past it by sliding the window to the run's last txn.  ow1: the op
+  // word (origin_left agent | origin_right agent << 16) every later txn must carry.  Returns the
+  // run's txns (>= 1) and, in `total`, their total length.  nv == 0: a generated op (no window).
+  CRDT_HD u32 typing_run(u32 b0, u32 nv, u32 remote, u32 agent, u32 ow1, const Rec& o, u32& total) {
     u32 nt = 1u;
-    total = o.w3;  // (a generated op: nv == 0, no record window to scan)
-    if (nv) nt = w.typing_scan(b0, nv, remote, agent, o.w1, o.w3, total);
-    // The run may go on past the window: slide the window to its last txn and scan on.
+    total = remote ? (o.w0 & 0x0FFFFFFFu) : o.w3;
+    if (!nv) return nt;
+    nt = w.typing_scan(b0, nv, remote, agent, ow1, o.w3, total);
     u32 per = remote ? 3u : 2u, rn = rec_n();
     u32 pos0 = g(T_RB_BASE) + b0;
-    while ((nv != 0u) & (pos0 + (nt + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
+    while ((pos0 + (nt + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
       u32 last = pos0 + (nt - 1u) * per;
       rec_window(last);
       nv = rn - last < 64u ? rn - last : 64u;
       u32 t2;
-      u32 n2 = w.typing_scan(0u, nv, remote, agent, o.w1, o.w3, t2);
+      u32 n2 = w.typing_scan(0u, nv, remote, agent, ow1, o.w3, t2);
       if (n2 <= 1u) break;
       total += t2 - w.rec_get(0u).w3;
       nt += n2 - 1u;
     }
+    return nt;
+  }
+  CRDT_HD u32 fast_typing(u32 b0, u32 nv, u32 remote, u32 idx, u32 orr, u32 agent, const Rec& o, u32 first) {
+    Span e = w.cget(idx);
+    if (!((e.len > 0) & (e.order + (u32)e.len == first) & (e.orr == orr))) return 0;
+    u32 total;
+    u32 nt = typing_run(b0, nv, remote, agent, o.w1, o, total);
     if (g(K_MAP) - first < total) return 0;     // capacity: the general path stops exactly
     w.fill(lof() + first, total, g(C_LEAF));   // notify (doc.rs:143-153)
     e.len += (i32)total;
     set(idx, e);
     inc(S_N_ITEMS, total);
     fast_txn_commit(first, total);
-    return nt * per;
+    return nt * (remote ? 3u : 2u);
   }
   // Delete `l` items at offset `off` of visible entry idx of the cached leaf: mutate_entry
   // (mutations.rs:227-277) and insert_internal's prepend / shift (mutations.rs:84-146) without a
@@ -1372,9 +1380,13 @@ struct Replayer {
       prof_cat = ((c.off == el) & can_append(e, item)) ? 0u : 3u;
 #endif
       if ((c.off == el) & can_append(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
+      // the typing that follows the inserted item appends to it: one entry for the whole run
+      u32 total;
+      u32 nt = typing_run(b0, nv, remote, agent, (agent & 0xFFFFu) | (o.w1 & 0xFFFF0000u), o, total);
+      item.len = (i32)total;
       if (!leaf_insert(idx, c.off, item)) return 0;
-      fast_txn_commit(first, l);
-      return per;
+      fast_txn_commit(first, total);
+      return nt * per;
     }
     i32 el = w.cget_len(idx);
     if ((el <= 0) | (c.off + l > (u32)el)) return 0;  // already deleted / spans entries
