@@ -1380,6 +1380,8 @@ struct Replayer {
       prof_cat = ((c.off == el) & can_append(e, item)) ? 0u : 3u;
 #endif
       if ((c.off == el) & can_append(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
+      // no room for the item (+ the entry's remainder): a leaf split, the general path's job
+      if (g(C_N) + 1u + (c.off < el) > (u32)L) return 0;
       // the typing that follows the inserted item appends to it: one entry for the whole run
       u32 total;
       u32 nt = typing_run(b0, nv, remote, agent, (agent & 0xFFFFu) | (o.w1 & 0xFFFF0000u), o, total);
