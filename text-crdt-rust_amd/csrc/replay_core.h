@@ -76,6 +76,11 @@ static_assert(N_SLOTS <= 128, "two context registers");
 template <class W, int L>
 struct Replayer {
   W w;  // owned by value: its lane registers stay SSA values, never a scratch object
+  // A one-insert txn the fast path resolved but could not place (its leaf must split): the item
+  // and the cursor after its origin_left, handed to apply_txn so it skips the op's lookups.
+  u32 pre = 0;
+  Span pre_item{0, 0, 0, 0};
+  Cursor pre_c{0, 0, 0};
 #ifdef CRDT_PROF
   u32 prof_cat = 0;  // diagnostic: which fast path ran (0 typing, 2 delete, 3 insert)
 #endif
@@ -881,6 +886,13 @@ struct Replayer {
     u32 remaining = 0, target = 0, lpos = 0, lins = 0;
     Span item{0, 0, 0, 0};
     Cursor c{0, 0, 0};
+    if (pre) {  // a fast-path attempt already resolved this one-insert txn (origins, cursor)
+      item = pre_item;
+      c = pre_c;
+      next = first + (u32)item.len;
+      k = 1;
+      mode = M_INS;
+    }
     while (true) {
       // ---------------------------------------------------------------- next op
       if (mode == M_FETCH) {
@@ -1381,7 +1393,12 @@ struct Replayer {
 #endif
       if ((c.off == el) & can_append(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
       // no room for the item (+ the entry's remainder): a leaf split, the general path's job
-      if (g(C_N) + 1u + (c.off < el) > (u32)L) return 0;
+      if (g(C_N) + 1u + (c.off < el) > (u32)L) {
+        pre = 1;
+        pre_item = item;
+        pre_c = c;
+        return 0;
+      }
       // the typing that follows the inserted item appends to it: one entry for the whole run
       u32 total;
       u32 nt = typing_run(b0, nv, remote, agent, (agent & 0xFFFFu) | (o.w1 & 0xFFFF0000u), o, total);
@@ -1439,6 +1456,7 @@ struct Replayer {
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
         consumed = gen ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, gen, gop) : ST_BAD_INPUT;
+        pre = 0;
 #ifdef CRDT_PROF
         inc(S_PROF1, (u32)(w.clock() - t1));
 #endif
