@@ -1240,6 +1240,16 @@ struct Replayer {
   CRDT_HD u32 fast_deletes(u32 b0, u32 nv, u32 remote, u32 agent, u32 idx, u32 off, u32 l, u32 first, const Rec& o) {
     u32 per = remote ? 3u : 2u;
     u32 t1 = w.cget_order(idx) + off;
+    if (g(C_N) + 2u > (u32)L) {  // near-full leaf: does the first delete fit (leaf_delete's rule)?
+      Span e = w.cget(idx);
+      u32 n = g(C_N), ha = off > 0u, hc = off + l < (u32)e.len, m = ha + hc;
+      if (m && idx + 1u < n) {
+        Span last = hc ? Span{t1 + l, t1 + l - 1u, e.orr, e.len - (i32)(off + l)}
+                       : Span{t1, ha ? t1 - 1u : e.ol, e.orr, -(i32)l};
+        m -= can_append(last, w.cget(idx + 1u));
+      }
+      if (n + m > (u32)L) return 0;  // a leaf split: the general path's job
+    }
     u32 k = 1, back = 0;
     u32 key = g(T_AGL_KEY);
     u32 in_run = !remote || (((o.w1 & 0xFFFFu) == agent) & (o.w2 - key < g(T_AGL_LEN)));
