@@ -101,6 +101,45 @@ def reduce_over_ranks(elapsed: float, digests: np.ndarray, dist, device):
     return float(t.item()), torch.cat(outs).cpu().numpy().view(np.uint64)
 
 
+def materialize_leg(eng, trace, n, hip, ev, s_, reps=5):
+    """Text materialisation, measured outside the timed step: every document
+    shares the trace's order-indexed content stream; k_materialize writes each document's text
+    from the published index.  Algorithmic bytes per document: canonical spans read (16 B) + vpos
+    read (4 B) per span, content read (4 B) + text written (4 B) per visible char.  Parity: every
+    document's text digest == the committed golden text digest (== the trace's endContent)."""
+    import ctypes as C
+    import json
+    from crdt_amd.traces import content_by_order, load_trace
+    eng.set_content(list(range(n)), [0] * n, [content_by_order(load_trace(trace))])
+    eng.materialize_async()
+    eng.sync()
+    ms = []
+    for _ in range(reps):
+        hip.hipEventRecord(ev[2], s_)
+        eng.materialize_async()
+        hip.hipEventRecord(ev[3], s_)
+        hip.hipEventSynchronize(ev[3])
+        x = C.c_float()
+        hip.hipEventElapsedTime(C.byref(x), ev[2], ev[3])
+        ms.append(x.value)
+    tdg = eng.text_digests()
+    e0 = eng.export(0)
+    lens = eng.lens()
+    canon_n = e0["canon"].shape[0]
+    alg = int(n * canon_n * 20 + int(lens.astype(np.int64).sum()) * 8)
+    k_ms = float(np.mean(ms))
+    gold = None
+    try:
+        gold = int(json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_golden.json")))[f"{trace}/L32"]["text_digest"], 16)
+    except (OSError, KeyError):
+        pass
+    return {"kernel": "k_materialize<32>", "kernel_ms": k_ms, "chars_per_s": float(lens.sum()) / (k_ms * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                         "frac": alg / (k_ms * 1e-3) / 1e9 / 8000.0, "alg_bytes_per_launch": alg},
+            "parity_ok": bool(gold is not None and (tdg == np.uint64(gold)).all()),
+            "parity": "every document's text digest == committed golden text digest (== endContent FNV, tests/golden)"}
+
+
 def golden_digest(trace: str):
     """Committed fixture (tests/golden/oracle_golden.json): the oracle's digest of the trace's
     remote replay with the release layout.  Every document of the bench must reproduce it."""
@@ -133,6 +172,7 @@ def main():
     ap.add_argument("--trace", default="automerge-paper")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-text", action="store_true", help="skip the text materialisation leg")
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
     args = ap.parse_args()
 
@@ -228,6 +268,7 @@ def main():
     t_max, all_dg = reduce_over_ranks(elapsed, dg, dist, dev)
     gold = golden_digest(args.trace)
     ok = ok and bool((all_dg == all_dg[0]).all()) and (gold is None or int(all_dg[0]) == gold)
+    mat = materialize_leg(eng, args.trace, n, hip, ev, s_) if not args.no_text else None
     total_ops = n_ops_doc * n * world * args.steps
     value = total_ops / t_max
     ms_step = t_max / args.steps * 1e3
@@ -273,6 +314,7 @@ def main():
             "parity_ok": ok,
             "parity": "every document's digest == committed oracle golden digest (tests/golden)",
             "stage_s": stage_s,
+            "materialize": mat,
         }
         print(json.dumps(out))
     if dist is not None:

@@ -139,6 +139,30 @@ int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
 int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint16_t* agent,
                               const uint32_t* seq, uint32_t* pos, uint8_t* deleted);
 
+/* ---- text materialisation (the reference's USE_INNER_ROPE rope) ----------
+ * The reference's rope (doc.rs:14-17, 59, 98 of list/mod.rs) receives the inserted string at
+ * cursor.count_pos() on every integrate (doc.rs:230-233) and loses the deleted visible range on
+ * every local delete (doc.rs:430-432); its remote-delete arm is todo!() (doc.rs:329-333), and
+ * ListCRDT::to_string returns it (doc.rs:498-505).  Here the rope is computed from the published
+ * index instead: the visible items in document order, each replaced by its code point.
+ *
+ * Content is an order-indexed UTF-32 table per document: content[order] is the code point of the
+ * item with that order (orders are assigned as in assign_order_to_client, doc.rs:155-165: within a
+ * txn, op by op, a LocalOp's deleted orders first, then its inserted chars).  Entries at delete
+ * orders are never read.  Streams are shared: document docs[i] reads stream stream_of_doc[i] =
+ * content[stream_off[k] .. stream_off[k+1]).  A call replaces all content set before. */
+int crdt_set_content(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* stream_of_doc,
+                     uint32_t n_streams, const uint64_t* stream_off, const uint32_t* content);
+/* Write every document's text on the device (publishes first if needed; stream-ordered). */
+int crdt_materialize_async(crdt_engine* e);
+/* ListCRDT::to_string (doc.rs:498-505) as UTF-32: *n_out = visible chars; out may be NULL (size
+ * query), else cap >= *n_out.  CRDT_E_ARG if the document has no content or its stream is shorter
+ * than the document's orders, or if it is poisoned. */
+int crdt_text(crdt_engine* e, uint32_t doc, uint32_t* out, uint64_t cap, uint64_t* n_out);
+/* Per-document 64-bit digest of the text (same as the oracle's text_digest; 0 = not materialised). */
+int crdt_text_digest(crdt_engine* e, uint64_t* per_doc /* n_docs */);
+int crdt_last_materialize_ms(crdt_engine* e, double* ms);
+
 /* ListCRDT::len (doc.rs:484-486) */
 int crdt_doc_len(crdt_engine* e, uint64_t n, const uint32_t* doc, uint32_t* len);
 int crdt_doc_status(crdt_engine* e, int32_t* status /* n_docs */);

@@ -984,6 +984,27 @@ inline u64 elem_hash(u32 section, u64 idx, u64 a, u64 b) {
   u64 k = mix64(((u64)section << 56) ^ idx);
   return mix64(mix64(k ^ a) ^ b);
 }
+// Text of a document (ListCRDT::to_string with USE_INNER_ROPE on, doc.rs:498-505): the rope gets
+// the inserted string at cursor.count_pos() (doc.rs:230-233) and loses each deleted visible range
+// (doc.rs:430-432), so it always equals the visible items in document order, each replaced by its
+// code point.  `content` is order-indexed (doc.rs:155-165 order assignment).  Returns false if the
+// table is shorter than the document's orders.
+inline bool text_of(const Doc& d, const u32* content, u64 clen, std::vector<u32>& out) {
+  out.clear();
+  if (clen < d.next_order()) return false;
+  std::vector<Span> raw;
+  std::vector<u32> ls;
+  d.raw_entries(raw, ls);
+  for (const Span& e : raw)
+    for (i32 i = 0; i < e.len; i++) out.push_back(content[e.order + (u32)i]);
+  return true;
+}
+inline u64 text_digest(const std::vector<u32>& t) {  // identical to k_materialize
+  u64 h = 0;
+  for (size_t p = 0; p < t.size(); p++) h += mix64(((u64)p << 32 | t[p]) ^ 0x5445585444494731ull);
+  return mix64(h ^ ((u64)t.size() << 32 | 0x54ull));
+}
+
 inline u64 digest(const Doc& d) {
   std::vector<Span> canon;
   d.canonical(canon);

@@ -246,6 +246,19 @@ void orc_loc_to_pos(void* h, uint32_t n, const uint16_t* agent, const uint32_t* 
   }
 }
 
+// Text (UTF-32) of the document from an order-indexed content table; returns its length, -1 if
+// the table is too short, -2 if out is too small.  out may be NULL (length only).
+int64_t orc_text(void* h, const uint32_t* content, uint64_t clen, uint32_t* out, uint64_t cap, uint64_t* digest_out) {
+  std::vector<u32> t;
+  if (!text_of(*(Doc*)h, content, clen, t)) return -1;
+  if (digest_out) *digest_out = text_digest(t);
+  if (out) {
+    if (cap < t.size()) return -2;
+    std::memcpy(out, t.data(), t.size() * 4);
+  }
+  return (int64_t)t.size();
+}
+
 // stats: [q2_triggers, integrate_iters, n_leaves]
 void orc_stats(void* h, uint64_t* s) {
   Doc* d = (Doc*)h;

@@ -53,6 +53,8 @@ def lib():
     L.orc_pos_to_loc.argtypes = [vp, u32, P(u32), P(u16), P(u32)]
     L.orc_loc_to_pos.argtypes = [vp, u32, P(u16), P(u32), P(u32), P(C.c_uint8)]
     L.orc_stats.argtypes = [vp, P(u64)]
+    L.orc_text.argtypes = [vp, P(u32), u64, P(u32), u64, P(u64)]
+    L.orc_text.restype = i64
     L.orc_dd_new.restype = vp
     L.orc_dd_free.argtypes = [vp]
     L.orc_dd_increment.argtypes = [vp, u32, u32]
@@ -147,6 +149,17 @@ class OracleDoc:
         self.L.orc_export(self.h, _p(raw), _p(ls), _p(canon), _p(cwo), _p(dels), _p(dd), _p(txn), _p(par), _p(fr))
         return dict(raw=raw, leaf_sizes=ls, canon=canon, cwo=cwo, deletes=dels, dd=dd, txns=txn,
                     parents=par, frontier=fr, len=s["len"], next_order=s["next_order"])
+
+    def text(self, content):
+        """(UTF-32 text, text digest) from an order-indexed content table (crdt_oracle.hpp text_of)."""
+        c = np.ascontiguousarray(content, dtype=np.uint32)
+        dg = np.zeros(1, np.uint64)
+        n = self.L.orc_text(self.h, _p(c), c.shape[0], None, 0, _p(dg, C.c_uint64))
+        if n < 0:
+            raise ValueError("content table shorter than the document's orders")
+        out = np.zeros(n, np.uint32)
+        self.L.orc_text(self.h, _p(c), c.shape[0], _p(out), n, None)
+        return out, int(dg[0])
 
     def pos_to_loc(self, pos):
         p = np.ascontiguousarray(pos, dtype=np.uint32)

@@ -250,3 +250,18 @@ def test_generator_invariants():
     # make_random_change keeps the document short (deletes of up to 10 chars outweigh inserts)
     assert len(d) <= 200
     assert s["next_order"] > 20000   # deletes of 1..10 chars consume several orders each
+
+
+@pytest.mark.parametrize("name", ["automerge-paper", "rustcode", "sveltecomponent"])
+@pytest.mark.parametrize("leaf,node", [(32, 16), (4, 8)])
+def test_text_matches_end_content(name, leaf, node):
+    # Text materialisation (to_string with the rope on, doc.rs:498-505) pinned by the reference's
+    # own fixture: the visible items' content in document order is the trace's endContent.
+    from crdt_amd.traces import content_by_order, fnv1a64, utf32_to_str
+    t = load_trace(name)
+    o = OracleDoc(leaf, node)
+    assert o.apply_trace(o.agent("a"), t.counts, t.patches) == 0
+    txt, _ = o.text(content_by_order(t))
+    b = utf32_to_str(txt).encode()
+    assert len(txt) == t.end_len and len(b) == t.end_bytes
+    assert fnv1a64(b) == t.end_fnv

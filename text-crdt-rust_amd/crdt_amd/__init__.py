@@ -100,6 +100,11 @@ def lib():
     L.crdt_last_timings.argtypes = [vp, P(C.c_double), P(C.c_double)]
     L.crdt_stream.argtypes = [vp]
     L.crdt_stream.restype = vp
+    L.crdt_set_content.argtypes = [vp, u64, P(u32), P(u32), u32, P(u64), P(u32)]
+    L.crdt_materialize_async.argtypes = [vp]
+    L.crdt_text.argtypes = [vp, u32, P(u32), u64, P(u64)]
+    L.crdt_text_digest.argtypes = [vp, P(u64)]
+    L.crdt_last_materialize_ms.argtypes = [vp, P(C.c_double)]
     L.crdt_last_error.restype = C.c_char_p
     _lib = L
     return L
@@ -112,7 +117,8 @@ EXPORTED_SYMBOLS = [
     "crdt_sync", "crdt_pos_to_loc", "crdt_loc_to_pos", "crdt_pos_to_loc_dev_async", "crdt_loc_to_pos_dev_async",
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
-    "crdt_stage_local_shared",
+    "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
+    "crdt_last_materialize_ms",
 ]
 
 
@@ -314,6 +320,37 @@ class Engine:
         return dict(raw=raw, leaf_sizes=ls, canon=canon, cwo=cwo, deletes=dl, dd=dd, txns=tx, parents=pa,
                     frontier=fr, len=n[11], next_order=n[10])
 
+    # --- text materialisation (ListCRDT::to_string with the rope on, doc.rs:498-505)
+    def set_content(self, docs: Sequence[int], stream_of_doc: Sequence[int], streams: Sequence[np.ndarray]):
+        """docs[i] reads the order-indexed UTF-32 table streams[stream_of_doc[i]]."""
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        so = np.ascontiguousarray(stream_of_doc, dtype=np.uint32)
+        off = np.concatenate([[0], np.cumsum([len(x) for x in streams])]).astype(np.uint64)
+        data = np.ascontiguousarray(np.concatenate([np.asarray(x, np.uint32) for x in streams])
+                                    if streams else np.zeros(0, np.uint32))
+        _check(self.L.crdt_set_content(self.h, d.shape[0], _p(d), _p(so), len(streams), _p(off, C.c_uint64),
+                                       _p(data)), "set_content")
+
+    def materialize_async(self):
+        _check(self.L.crdt_materialize_async(self.h), "materialize")
+
+    def text(self, doc: int) -> np.ndarray:
+        n = C.c_uint64()
+        _check(self.L.crdt_text(self.h, doc, None, 0, C.byref(n)), "text")
+        out = np.zeros(n.value, np.uint32)
+        _check(self.L.crdt_text(self.h, doc, _p(out), n.value, C.byref(n)), "text")
+        return out
+
+    def text_digests(self) -> np.ndarray:
+        out = np.zeros(self.n_docs, np.uint64)
+        _check(self.L.crdt_text_digest(self.h, _p(out, C.c_uint64)), "text_digest")
+        return out
+
+    def materialize_ms(self) -> float:
+        x = C.c_double()
+        self.L.crdt_last_materialize_ms(self.h, C.byref(x))
+        return x.value
+
     def timings(self):
         a, b = C.c_double(), C.c_double()
         self.L.crdt_last_timings(self.h, C.byref(a), C.byref(b))
@@ -343,6 +380,13 @@ class ListCRDT:
 
     def apply_remote_wire(self, wire: bytes) -> int:            # doc.rs:242 (batch of RemoteTxn)
         return int(self.e.apply_remote_wire([0], [wire])[0])
+
+    def set_content(self, content: np.ndarray):
+        self.e.set_content([0], [0], [content])
+
+    def to_string(self) -> str:                                 # doc.rs:498-505 (rope on)
+        from .traces import utf32_to_str
+        return utf32_to_str(self.e.text(0))
 
     def __len__(self) -> int:                                   # doc.rs:484
         return int(self.e.lens([0])[0])

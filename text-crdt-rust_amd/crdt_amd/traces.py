@@ -65,3 +65,34 @@ def load_remote_wire(name: str, data_dir: str = DATA_DIR) -> bytes:
     tests/golden/make_remote.py (see include/crdt_gpu.h "Remote wire batch")."""
     with gzip.open(os.path.join(data_dir, name + ".rtx.gz"), "rb") as f:
         return f.read()
+
+
+def content_by_order(t: Trace) -> np.ndarray:
+    """Order-indexed UTF-32 content of a trace replayed as one agent's local txns (or their remote
+    form): orders are assigned per LocalOp, deleted orders first, then the inserted chars
+    (doc.rs:155-165, 376-469).  Entries at delete orders are 0 (never read)."""
+    cps = np.frombuffer(t.text.decode("utf-8").encode("utf-32-le"), dtype="<u4").astype(np.uint32)
+    dl = t.patches[:, 1].astype(np.int64)
+    ins = t.patches[:, 2].astype(np.int64)
+    start = np.concatenate([[0], np.cumsum(dl + ins)[:-1]]) + dl       # first inserted order per patch
+    n_ins = int(ins.sum())
+    if cps.shape[0] != n_ins:
+        raise ValueError(f"{t.name}: {cps.shape[0]} inserted code points, patches say {n_ins}")
+    ins_excl = np.concatenate([[0], np.cumsum(ins)[:-1]])
+    orders = np.repeat(start, ins) + (np.arange(n_ins) - np.repeat(ins_excl, ins))
+    out = np.zeros(t.n_orders, np.uint32)
+    out[orders] = cps
+    return out
+
+
+def utf32_to_str(a: np.ndarray) -> str:
+    return np.ascontiguousarray(a, dtype="<u4").tobytes().decode("utf-32-le")
+
+
+def fnv1a64(b: bytes) -> int:
+    """FNV-1a over bytes (the trace header's end_fnv of endContent, tests/golden/make_traces.py)."""
+    h = 0xCBF29CE484222325
+    a = np.frombuffer(b, dtype=np.uint8)
+    for x in a.tolist():
+        h = ((h ^ x) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h

@@ -81,7 +81,7 @@ struct crdt_engine {
   u32 L = 32;
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   u64 n_docs = 0;
   std::vector<DocHost> docs;
   std::vector<DocSeg> seg_h;
@@ -99,7 +99,19 @@ struct crdt_engine {
   Rec* recs = nullptr;
   u64 rec_cap = 0;
   bool published = false;
-  double last_replay_ms = 0, last_publish_ms = 0;
+  double last_replay_ms = 0, last_publish_ms = 0, last_materialize_ms = 0;
+  // text materialisation: order-indexed content streams, per-document stream offsets, output text
+  u32* content = nullptr;
+  u64 content_cap = 0;
+  std::vector<u64> cbase_h, clen_h;
+  u64* cbase = nullptr;
+  u64* clen = nullptr;
+  u32* text = nullptr;
+  u64 text_cap = 0;
+  u64 map_total = 0;
+  u32* tlen = nullptr;
+  u64* tdigest = nullptr;
+  bool materialized = false;
   // query scratch
   void* qbuf = nullptr;
   u64 qbuf_bytes = 0;
@@ -141,6 +153,10 @@ struct crdt_engine {
     dfree(st); dfree(segs); dfree(frontier); dfree(groups); dfree(canon_n); dfree(len); dfree(digest); dfree(n_agents_d);
     dfree(recs);
     rec_cap = 0;
+    dfree(content); dfree(cbase); dfree(clen); dfree(text); dfree(tlen); dfree(tdigest);
+    content_cap = 0;
+    text_cap = 0;
+    materialized = false;
     if (qbuf) (void)hipFree(qbuf);
     qbuf = nullptr;
     qbuf_bytes = 0;
@@ -168,6 +184,14 @@ struct crdt_engine {
     HIPCHK(dalloc(len, n));
     HIPCHK(dalloc(digest, n));
     HIPCHK(dalloc(n_agents_d, n));
+    HIPCHK(dalloc(cbase, n));
+    HIPCHK(dalloc(clen, n));
+    HIPCHK(dalloc(tlen, n));
+    HIPCHK(dalloc(tdigest, n));
+    cbase_h.assign(n, NO_CONTENT);
+    clen_h.assign(n, 0);
+    HIPCHK(hipMemsetAsync(cbase, 0xFF, sizeof(u64) * std::max<u64>(n, 1), stream));
+    HIPCHK(hipMemsetAsync(clen, 0, sizeof(u64) * std::max<u64>(n, 1), stream));
     HIPCHK(hipMemsetAsync(st, 0, sizeof(DocState) * std::max<u64>(n, 1), stream));
     // size every document for an empty stream and initialise it
     for (u64 d = 0; d < n; d++) docs[d].caps = plan_caps(StreamNeeds{}, 0, true, 48);
@@ -260,7 +284,9 @@ struct crdt_engine {
     pools.free_all();
     pools = np;
     seg_h = nseg;
+    map_total = nm;
     published = false;
+    materialized = false;
     return 0;
   }
 
@@ -275,6 +301,7 @@ struct crdt_engine {
       HIPCHK(hipGetLastError());
     }
     published = false;
+    materialized = false;
     return 0;
   }
 
@@ -384,6 +411,7 @@ struct crdt_engine {
     }
     HIPCHK(hipStreamSynchronize(stream));
     published = false;
+    materialized = false;
     return 0;
   }
 
@@ -394,6 +422,7 @@ struct crdt_engine {
     else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
     HIPCHK(hipGetLastError());
     published = false;
+    materialized = false;
     return 0;
   }
 
@@ -460,6 +489,7 @@ struct crdt_engine {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev[3], stream));
     published = true;
+    materialized = false;
     return 0;
   }
   int ensure_published() {
@@ -470,6 +500,81 @@ struct crdt_engine {
     float ms = 0;
     (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
     last_publish_ms = ms;
+    return 0;
+  }
+  TextIO text_view() const {
+    TextIO t{};
+    t.content = content;
+    t.cbase = cbase;
+    t.clen = clen;
+    t.text = text;
+    t.tlen = tlen;
+    t.tdigest = tdigest;
+    return t;
+  }
+  // Content streams (order-indexed UTF-32); document docs[i] reads stream stream_of_doc[i].
+  // Replaces all previously set content; documents not named have none.
+  int set_content(u64 n, const uint32_t* docs, const uint32_t* stream_of_doc, u32 n_streams, const uint64_t* stream_off,
+                  const uint32_t* data) {
+    int r = set_device();
+    if (r) return r;
+    for (u32 k = 0; k < n_streams; k++)
+      if (stream_off[k + 1] < stream_off[k]) return CRDT_E_ARG;
+    for (u64 i = 0; i < n; i++)
+      if (docs[i] >= n_docs || stream_of_doc[i] >= n_streams) return CRDT_E_ARG;
+    u64 total = stream_off[n_streams];
+    HIPCHK(hipStreamSynchronize(stream));
+    if (total > content_cap) {
+      dfree(content);
+      HIPCHK(dalloc(content, total));
+      content_cap = std::max<u64>(total, 1);
+    }
+    if (total) HIPCHK(hipMemcpyAsync(content, data, total * 4, hipMemcpyHostToDevice, stream));
+    std::fill(cbase_h.begin(), cbase_h.end(), NO_CONTENT);
+    std::fill(clen_h.begin(), clen_h.end(), 0);
+    for (u64 i = 0; i < n; i++) {
+      u32 k = stream_of_doc[i];
+      cbase_h[docs[i]] = stream_off[k];
+      clen_h[docs[i]] = stream_off[k + 1] - stream_off[k];
+    }
+    HIPCHK(hipMemcpyAsync(cbase, cbase_h.data(), n_docs * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(clen, clen_h.data(), n_docs * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    materialized = false;
+    return 0;
+  }
+  int materialize() {
+    int r = set_device();
+    if (r) return r;
+    if (!n_docs) return 0;
+    if (!published) {
+      r = publish();
+      if (r) return r;
+    }
+    if (text_cap < map_total) {
+      HIPCHK(hipStreamSynchronize(stream));
+      dfree(text);
+      HIPCHK(dalloc(text, map_total));
+      text_cap = std::max<u64>(map_total, 1);
+    }
+    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    HIPCHK(hipEventRecord(ev[4], stream));
+    if (L == 32) hipLaunchKernelGGL(k_materialize<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), text_view(), (u32)n_docs);
+    else hipLaunchKernelGGL(k_materialize<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), text_view(), (u32)n_docs);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev[5], stream));
+    materialized = true;
+    return 0;
+  }
+  int ensure_materialized() {
+    if (!materialized) {
+      int r = materialize();
+      if (r) return r;
+    }
+    HIPCHK(hipStreamSynchronize(stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, ev[4], ev[5]);
+    last_materialize_ms = ms;
     return 0;
   }
   int scratch(u64 bytes) {
@@ -898,6 +1003,46 @@ int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms) {
 }
 
 void* crdt_stream(crdt_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int crdt_set_content(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* stream_of_doc,
+                     uint32_t n_streams, const uint64_t* stream_off, const uint32_t* content) {
+  if (!valid(e) || (n_docs && (!docs || !stream_of_doc)) || !stream_off || (stream_off[n_streams] && !content))
+    return CRDT_E_ARG;
+  return e->set_content(n_docs, docs, stream_of_doc, n_streams, stream_off, content);
+}
+
+int crdt_materialize_async(crdt_engine* e) {
+  if (!valid(e)) return CRDT_E_ARG;
+  return e->materialize();
+}
+
+int crdt_text(crdt_engine* e, uint32_t doc, uint32_t* out, uint64_t cap, uint64_t* n_out) {
+  if (!valid(e) || doc >= e->n_docs || !n_out) return CRDT_E_ARG;
+  int r = e->ensure_materialized();
+  if (r) return r;
+  u32 n = 0;
+  HIPCHK(hipMemcpy(&n, e->tlen + doc, 4, hipMemcpyDeviceToHost));
+  if (n == INVALID) return CRDT_E_ARG;  // no (or too short) content for this document
+  *n_out = n;
+  if (!out) return 0;
+  if (cap < n) return CRDT_E_ARG;
+  if (n) HIPCHK(hipMemcpy(out, e->text + e->seg_h[doc].map_base, (u64)n * 4, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int crdt_text_digest(crdt_engine* e, uint64_t* per_doc) {
+  if (!valid(e) || !per_doc) return CRDT_E_ARG;
+  int r = e->ensure_materialized();
+  if (r) return r;
+  HIPCHK(hipMemcpy(per_doc, e->tdigest, e->n_docs * 8, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int crdt_last_materialize_ms(crdt_engine* e, double* ms) {
+  if (!e || !ms) return CRDT_E_ARG;
+  *ms = e->last_materialize_ms;
+  return 0;
+}
 
 const char* crdt_last_error(void) { return g_last_error.c_str(); }
 

@@ -249,6 +249,89 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Text materialisation.  The reference keeps a rope in step with the tree when
+// USE_INNER_ROPE is on: insert the content at cursor.count_pos() (doc.rs:230-233), remove the
+// deleted visible range (doc.rs:430-432; the remote delete arm is todo!() at doc.rs:329-333).
+// The rope therefore always equals "content of the visible items in document order", which is
+// what this kernel writes from the published index: for canonical span k with len > 0,
+// text[vpos[k] + i] = content[order_k + i].  Content is an order-indexed UTF-32 table (entries at
+// delete orders are never read).
+// ---------------------------------------------------------------------------------------------
+#define NO_CONTENT 0xFFFFFFFFFFFFFFFFull
+
+struct TextIO {
+  const u32* content;  // order-indexed code points: document d reads content[cbase[d] + order]
+  const u64* cbase;    // [doc] (NO_CONTENT: no content staged)
+  const u64* clen;     // [doc] entries available from cbase
+  u32* text;           // [map_base + pos]
+  u32* tlen;           // [doc] visible chars written, INVALID if not materialised
+  u64* tdigest;        // [doc] text digest (0 if not materialised)
+};
+
+// text digest, identical in oracle/crdt_oracle.hpp (text_digest)
+__device__ __forceinline__ u64 text_hash(u32 pos, u32 cp) { return mix64(((u64)pos << 32 | cp) ^ 0x5445585444494731ull); }
+
+// One wave per document.  64 canonical spans at a time: a prefix scan of their visible lengths
+// gives each output position j of the chunk; lane l owns positions t+l and finds its span by a
+// 6-step search over the scan (bpermute), so stores are fully coalesced (contiguous positions)
+// and loads are contiguous within a span.  U positions per lane are in flight per step.
+template <int L>
+__global__ __launch_bounds__(256) void k_materialize(Pools P, PubOut O, TextIO T, u32 n) {
+  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
+  if (d >= n) return;
+  u32 l = lane_id();
+  i32 stt = P.st[d].status;
+  u32 next_order = P.st[d].next_order;
+  u64 cb = T.cbase[d], cl = T.clen[d];
+  if ((stt != ST_OK && stt != ST_NEED_CAPACITY) || cb == NO_CONTENT || cl < (u64)next_order) {
+    if (l == 0) { T.tlen[d] = INVALID; T.tdigest[d] = 0; }
+    return;
+  }
+  DocSeg seg = P.seg[d];
+  const Span* cn = O.canon + seg.leaf_base * L;
+  const u32* vp = O.vpos + seg.leaf_base * L;
+  u32 ns = O.canon_n[d];
+  const u32* src = T.content + cb;
+  u32* dst = T.text + seg.map_base;
+  constexpr u32 U = 4;
+  u64 h = 0;
+  for (u32 k0 = 0; k0 < ns; k0 += 64) {
+    u32 k = k0 + l;
+    Span sp = k < ns ? cn[k] : Span{0, 0, 0, 0};
+    u32 ln = sp.len > 0 ? (u32)sp.len : 0u;
+    u32 base = uni(vp[k0]);
+    u32 Pi = wave_incl_scan(ln);
+    u32 Tn = rdlane(Pi, 63);
+    for (u32 t = 0; t < Tn; t += 64 * U) {
+      u32 cp[U], jj[U];
+#pragma unroll
+      for (u32 u = 0; u < U; u++) {
+        u32 j = t + u * 64 + l;
+        u32 m = 0;
+        for (u32 step = 32; step; step >>= 1)
+          if (shfl(Pi, m + step - 1u) <= j) m += step;  // m = lanes whose prefix ends at or before j
+        u32 pm = shfl(Pi, m), lm = shfl(ln, m), om = shfl(sp.order, m);
+        jj[u] = j;
+        cp[u] = j < Tn ? src[om + (j - (pm - lm))] : 0u;
+      }
+#pragma unroll
+      for (u32 u = 0; u < U; u++) {
+        if (jj[u] < Tn) {
+          dst[base + jj[u]] = cp[u];
+          h += text_hash(base + jj[u], cp[u]);
+        }
+      }
+    }
+  }
+  h = wave_sum64(h);
+  if (l == 0) {
+    u32 len = O.len[d];
+    T.tlen[d] = len;
+    T.tdigest[d] = mix64(h ^ ((u64)len << 32 | 0x54ull));
+  }
+}
+
 template <class T>
 __device__ __forceinline__ i32 find_run(const T* b, u32 n, u32 x) {  // simple_rle.rs:18-25 search
   u32 lo = 0, hi = n;
