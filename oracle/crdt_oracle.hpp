@@ -999,9 +999,14 @@ inline bool text_of(const Doc& d, const u32* content, u64 clen, std::vector<u32>
     for (i32 i = 0; i < e.len; i++) out.push_back(content[e.order + (u32)i]);
   return true;
 }
-inline u64 text_digest(const std::vector<u32>& t) {  // identical to k_materialize
+inline u64 text_digest(const std::vector<u32>& t) {  // identical to k_materialize (text_hash)
   u64 h = 0;
-  for (size_t p = 0; p < t.size(); p++) h += mix64(((u64)p << 32 | t[p]) ^ 0x5445585444494731ull);
+  for (size_t p = 0; p < t.size(); p++) {
+    u32 x = ((u32)p * 0x9E3779B1u) ^ t[p];
+    x ^= x >> 16; x *= 0x85EBCA6Bu;
+    x ^= x >> 13; x *= 0xC2B2AE35u;
+    h += x ^ (x >> 16);
+  }
   return mix64(h ^ ((u64)t.size() << 32 | 0x54ull));
 }
 

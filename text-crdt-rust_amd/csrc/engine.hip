@@ -557,10 +557,9 @@ struct crdt_engine {
       HIPCHK(dalloc(text, map_total));
       text_cap = std::max<u64>(map_total, 1);
     }
-    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     HIPCHK(hipEventRecord(ev[4], stream));
-    if (L == 32) hipLaunchKernelGGL(k_materialize<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), text_view(), (u32)n_docs);
-    else hipLaunchKernelGGL(k_materialize<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), text_view(), (u32)n_docs);
+    if (L == 32) hipLaunchKernelGGL(k_materialize<32>, dim3((u32)n_docs), dim3(64 * MAT_WAVES), 0, stream, pools_view(pools), pub_view(), text_view(), (u32)n_docs);
+    else hipLaunchKernelGGL(k_materialize<4>, dim3((u32)n_docs), dim3(64 * MAT_WAVES), 0, stream, pools_view(pools), pub_view(), text_view(), (u32)n_docs);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev[5], stream));
     materialized = true;

@@ -5,6 +5,7 @@
 //   k_publish   flat index build: canonical spans (can_append compaction of the leaf entries in
 //               document order), visible-prefix vpos, order->span scatter, digest
 //   k_pos_to_loc / k_loc_to_pos   batched lookups on the published index (thread per query)
+//   k_materialize  document text from the published index + content streams (block per document)
 #pragma once
 #include "replay_core.h"
 #include "wave_gpu.h"
@@ -269,23 +270,35 @@ struct TextIO {
   u64* tdigest;        // [doc] text digest (0 if not materialised)
 };
 
-// text digest, identical in oracle/crdt_oracle.hpp (text_digest)
-__device__ __forceinline__ u64 text_hash(u32 pos, u32 cp) { return mix64(((u64)pos << 32 | cp) ^ 0x5445585444494731ull); }
+// text digest, identical in oracle/crdt_oracle.hpp (text_digest): a 32-bit murmur3 finaliser per
+// (position, code point), summed in 64 bits, mixed once at the end (full-rate-friendly: two 32-bit
+// multiplies per char instead of a 64-bit splitmix)
+__device__ __forceinline__ u32 text_hash(u32 pos, u32 cp) {
+  u32 h = (pos * 0x9E3779B1u) ^ cp;
+  h ^= h >> 16; h *= 0x85EBCA6Bu;
+  h ^= h >> 13; h *= 0xC2B2AE35u;
+  return h ^ (h >> 16);
+}
 
-// One wave per document.  64 canonical spans at a time: a prefix scan of their visible lengths
-// gives each output position j of the chunk; lane l owns positions t+l and finds its span by a
-// 6-step search over the scan (bpermute), so stores are fully coalesced (contiguous positions)
-// and loads are contiguous within a span.  U positions per lane are in flight per step.
+// One block (MAT_WAVES waves) per document; wave w takes chunks w, w+MAT_WAVES, ... of 64
+// canonical spans (each chunk's output starts at vpos[k0], so chunks are independent).  Within a
+// chunk a prefix scan of the visible lengths gives each output position j; lane l owns positions
+// t+l and finds its span by a 6-step search over the scan (bpermute), so stores are fully
+// coalesced (contiguous positions) and loads are contiguous within a span.  U positions per lane
+// are in flight per step.
+#define MAT_WAVES 4
 template <int L>
-__global__ __launch_bounds__(256) void k_materialize(Pools P, PubOut O, TextIO T, u32 n) {
-  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
+__global__ __launch_bounds__(64 * MAT_WAVES) void k_materialize(Pools P, PubOut O, TextIO T, u32 n) {
+  u32 d = blockIdx.x;
   if (d >= n) return;
   u32 l = lane_id();
+  u32 wv = uni(threadIdx.x >> 6);
+  __shared__ u64 s_h[MAT_WAVES];
   i32 stt = P.st[d].status;
   u32 next_order = P.st[d].next_order;
   u64 cb = T.cbase[d], cl = T.clen[d];
   if ((stt != ST_OK && stt != ST_NEED_CAPACITY) || cb == NO_CONTENT || cl < (u64)next_order) {
-    if (l == 0) { T.tlen[d] = INVALID; T.tdigest[d] = 0; }
+    if (threadIdx.x == 0) { T.tlen[d] = INVALID; T.tdigest[d] = 0; }
     return;
   }
   DocSeg seg = P.seg[d];
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(256) void k_materialize(Pools P, PubOut O, TextIO T
   u32* dst = T.text + seg.map_base;
   constexpr u32 U = 4;
   u64 h = 0;
-  for (u32 k0 = 0; k0 < ns; k0 += 64) {
+  for (u32 k0 = wv * 64; k0 < ns; k0 += 64 * MAT_WAVES) {
     u32 k = k0 + l;
     Span sp = k < ns ? cn[k] : Span{0, 0, 0, 0};
     u32 ln = sp.len > 0 ? (u32)sp.len : 0u;
@@ -325,10 +338,14 @@ __global__ __launch_bounds__(256) void k_materialize(Pools P, PubOut O, TextIO T
     }
   }
   h = wave_sum64(h);
-  if (l == 0) {
+  if (l == 0) s_h[wv] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 hs = 0;
+    for (u32 w = 0; w < MAT_WAVES; w++) hs += s_h[w];
     u32 len = O.len[d];
     T.tlen[d] = len;
-    T.tdigest[d] = mix64(h ^ ((u64)len << 32 | 0x54ull));
+    T.tdigest[d] = mix64(hs ^ ((u64)len << 32 | 0x54ull));
   }
 }
 
