@@ -135,7 +135,8 @@ def materialize_leg(eng, trace, n, hip, ev, s_, reps=5):
         pass
     return {"kernel": "k_materialize<32>", "kernel_ms": k_ms, "chars_per_s": float(lens.sum()) / (k_ms * 1e-3),
             "roofline": {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                         "frac": alg / (k_ms * 1e-3) / 1e9 / 8000.0, "alg_bytes_per_launch": alg},
+                         "frac": alg / (k_ms * 1e-3) / 1e9 / 8000.0, "alg_bytes_per_launch": alg,
+                         "traffic": measured_traffic(n, "k_materialize")},
             "parity_ok": bool(gold is not None and (tdg == np.uint64(gold)).all()),
             "parity": "every document's text digest == committed golden text digest (== endContent FNV, tests/golden)"}
 
@@ -151,11 +152,11 @@ def golden_digest(trace: str):
         return None
 
 
-def measured_traffic(n_docs: int):
-    """HBM bytes per k_replay launch from the committed PMC pass (profiles/traffic_k_replay.json:
+def measured_traffic(n_docs: int, kernel: str = "k_replay"):
+    """HBM bytes per launch of `kernel` from the committed PMC pass (profiles/traffic_<kernel>.json:
     FETCH_SIZE x 2 + WRITE_SIZE per the MI355X guide's gfx950 correction), scaled per document."""
     import json
-    p = os.path.join(ROOT, "profiles", "traffic_k_replay.json")
+    p = os.path.join(ROOT, "profiles", f"traffic_{kernel}.json")
     try:
         t = json.load(open(p))
         return t["hbm_bytes_per_launch"] / t["docs"] * n_docs

@@ -9,22 +9,24 @@ import sys
 
 docs = int(sys.argv[1])
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/traffic_k_replay.json"
+kernel = sys.argv[3] if len(sys.argv) > 3 else "k_replay"
+tag = sys.argv[4] if len(sys.argv) > 4 else ""
 
 
 def last_value(pattern, counter):
     rows = []
     for f in glob.glob(pattern, recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_replay" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 rows.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     rows.sort()
     return rows[-1][1], len(rows)
 
 
-fetch_kb, nf = last_value("gpurun_out/pmc_fetch/**/*counter_collection.csv", "FETCH_SIZE")
-write_kb, nw = last_value("gpurun_out/pmc_write/**/*counter_collection.csv", "WRITE_SIZE")
+fetch_kb, nf = last_value(f"gpurun_out/pmc_fetch{tag}/**/*counter_collection.csv", "FETCH_SIZE")
+write_kb, nw = last_value(f"gpurun_out/pmc_write{tag}/**/*counter_collection.csv", "WRITE_SIZE")
 res = {
-    "kernel": "k_replay<32>", "docs": docs, "workload": "automerge-paper remote, one clean launch",
+    "kernel": kernel + "<32>", "docs": docs, "workload": "automerge-paper remote, one clean launch",
     "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
     "hbm_bytes_per_launch": fetch_kb * 1024 * 2 + write_kb * 1024,
     "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1",
