@@ -310,8 +310,9 @@ struct crdt_engine {
     std::vector<u32> na(n_docs);
     for (u64 d = 0; d < n_docs; d++) na[d] = (u32)docs[d].agents.names.size();
     HIPCHK(hipMemcpyAsync(n_agents_d, na.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
-    for (u64 d = 0; d < n_docs; d++) {
-      HIPCHK(hipMemcpyAsync((char*)(st + d) + offsetof(DocState, n_agents), n_agents_d + d, 4, hipMemcpyDeviceToDevice, stream));
+    if (n_docs) {  // one launch for every document (not one 4-byte copy per document)
+      hipLaunchKernelGGL(k_set_n_agents, dim3((u32)((n_docs + 255) / 256)), dim3(256), 0, stream, st, (const u32*)n_agents_d, (u32)n_docs);
+      HIPCHK(hipGetLastError());
     }
     return 0;
   }

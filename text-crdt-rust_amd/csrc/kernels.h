@@ -69,6 +69,12 @@ __global__ void k_reset_recpos(DocState* st, u32 n, u32 n_agents_dummy) {
   if (d < n) st[d].rec_pos = 0;
 }
 
+// Host-side agent counts into every document's state (before k_init / a replay).
+__global__ void k_set_n_agents(DocState* st, const u32* na, u32 n) {
+  u32 d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d < n) st[d].n_agents = na[d];
+}
+
 template <class T>
 __device__ __forceinline__ void bcopy(T* dst, const T* src, u64 n) {
   for (u64 k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
