@@ -1,4 +1,5 @@
-"""CPU-only checks of the C-ABI library: it loads, exports every symbol include/crdt_gpu.h declares,
+"""CPU-only checks of the C-ABI library: it loads, exports every symbol include/crdt_gpu.h and
+include/crdt_trace.h declare,
 and refuses to run without a gfx950 device (no silent CPU fallback)."""
 import ctypes
 import os
@@ -12,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    h = open(os.path.join(ROOT, "include", "crdt_gpu.h")).read()
+    h = "".join(open(os.path.join(ROOT, "include", f)).read() for f in ("crdt_gpu.h", "crdt_trace.h"))
     return sorted(set(re.findall(r"\b(crdt_[a-z_0-9]+)\s*\(", h)))
 
 

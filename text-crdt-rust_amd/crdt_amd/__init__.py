@@ -36,7 +36,8 @@ class CrdtError(RuntimeError):
 def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defines: Sequence[str] = ()) -> str:
     """Compile libcrdt_gpu.so for gfx950 with hipcc (in-tree).  `defines` only for diagnostic
     builds written to another `out` (e.g. CRDT_PROF)."""
-    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(INCLUDE, "crdt_gpu.h")]
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
+        os.path.join(INCLUDE, h) for h in ("crdt_gpu.h", "crdt_trace.h")]
     if not force and os.path.exists(out):
         lt = os.path.getmtime(out)
         if all(os.path.getmtime(s) <= lt for s in srcs):
@@ -44,7 +45,7 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defin
     os.makedirs(os.path.dirname(out), exist_ok=True)
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-fno-strict-aliasing", "-I" + INCLUDE, "-I" + CSRC, "-o", out + ".tmp"] + ["-D" + d for d in defines] + [
-           os.path.join(CSRC, "engine.hip")]
+           os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "trace_ingest.cpp"), "-lz"]
     r = subprocess.run(cmd, capture_output=not verbose, text=True)
     if r.returncode != 0:
         raise CrdtError("hipcc failed:\n" + (r.stderr or "")[-4000:])
@@ -106,6 +107,12 @@ def lib():
     L.crdt_text_digest.argtypes = [vp, P(u64)]
     L.crdt_last_materialize_ms.argtypes = [vp, P(C.c_double)]
     L.crdt_last_error.restype = C.c_char_p
+    L.crdt_trace_load.argtypes = [C.c_char_p, P(vp)]
+    L.crdt_trace_parse.argtypes = [C.c_char_p, u64, P(vp)]
+    L.crdt_trace_sizes.argtypes = [vp, P(u64)]
+    L.crdt_trace_copy.argtypes = [vp, vp, vp, C.c_char_p, C.c_char_p, C.c_char_p]
+    L.crdt_trace_free.argtypes = [vp]
+    L.crdt_trace_free.restype = None
     _lib = L
     return L
 
@@ -119,6 +126,8 @@ EXPORTED_SYMBOLS = [
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
     "crdt_last_materialize_ms",
+    # include/crdt_trace.h (host-only trace ingestion)
+    "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
 
 

@@ -2,7 +2,8 @@
 
 Mirrors crdt-testdata's `load_testing_data` (src/testdata/src/lib.rs:29-48): a trace is a list of
 txns, each a list of patches (pos, del_len, ins_content); positions count Unicode scalar values.
-The JSON->binary conversion is tests/golden/make_traces.py (run once in the build container).
+The JSON->binary conversion is tests/golden/make_traces.py (run once in the build container);
+`ingest_json` decodes a reference trace file (.json.gz) natively instead (include/crdt_trace.h).
 Only lengths of inserted strings are used by the CRDT hot path (doc.rs:383: chars().count()).
 """
 from __future__ import annotations
@@ -96,3 +97,33 @@ def fnv1a64(b: bytes) -> int:
     for x in a.tolist():
         h = ((h ^ x) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
     return h
+
+
+def ingest_json(path: str) -> Trace:
+    """Decode a reference trace file (gzip'd or plain JSON, schema src/testdata/src/lib.rs:10-27) with
+    the native streaming decoder of libcrdt_gpu.so (crdt_trace_load, include/crdt_trace.h), the
+    replacement of crdt-testdata `load_testing_data` (lib.rs:29-48).  Host-only; no GPU needed."""
+    import ctypes as C
+    from . import _check, lib
+
+    L = lib()
+    h = C.c_void_p()
+    _check(L.crdt_trace_load(os.fsencode(path), C.byref(h)), "crdt_trace_load")
+    try:
+        sz = np.zeros(7, np.uint64)
+        _check(L.crdt_trace_sizes(h, sz.ctypes.data_as(C.POINTER(C.c_uint64))), "crdt_trace_sizes")
+        n_txns, n_patches, text_b, start_len, start_b, end_len, end_b = (int(x) for x in sz)
+        counts = np.zeros(n_txns, np.uint32)
+        patches = np.zeros((n_patches, 3), np.uint32)
+        text = C.create_string_buffer(max(text_b, 1))
+        start = C.create_string_buffer(max(start_b, 1))
+        end = C.create_string_buffer(max(end_b, 1))
+        _check(L.crdt_trace_copy(h, counts.ctypes.data, patches.ctypes.data, text, start, end), "crdt_trace_copy")
+    finally:
+        L.crdt_trace_free(h)
+    end_bytes = end.raw[:end_b]
+    tr = Trace(os.path.basename(path).split(".")[0], counts, patches, start_len, end_len, end_b,
+               fnv1a64(end_bytes), text.raw[:text_b])
+    tr.start = start.raw[:start_b]
+    tr.end = end_bytes
+    return tr

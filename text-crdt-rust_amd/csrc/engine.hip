@@ -1047,3 +1047,9 @@ int crdt_last_materialize_ms(crdt_engine* e, double* ms) {
 const char* crdt_last_error(void) { return g_last_error.c_str(); }
 
 }  // extern "C"
+
+// Shared with the host-only sources (trace_ingest.cpp) so every entry point reports through
+// crdt_last_error().
+namespace crdt {
+void set_last_error(const std::string& s) { g_last_error = s; }
+}  // namespace crdt
