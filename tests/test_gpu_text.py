@@ -111,3 +111,25 @@ def test_text_errors():
     assert st[0] == 0
     e2.set_content([0], [0], [np.array([65, 66, 67], np.uint32)])
     assert utf32_to_str(e2.text(0)) == "ABC"
+
+
+def test_json_file_to_text(tmp_path):
+    # §8f row 4 end to end: a trace file in the reference's own format (gzip'd JSON, lib.rs:10-27)
+    # -> native decoder (crdt_trace_load) -> GPU replay -> GPU materialisation == endContent.
+    import gzip
+    import json
+    from crdt_amd.traces import ingest_json
+    from test_trace_ingest import _replay_text, _to_json_obj
+    t = load_trace("sveltecomponent")
+    p = tmp_path / "sveltecomponent.json.gz"
+    with gzip.open(p, "wt", encoding="utf-8") as f:
+        json.dump(_to_json_obj(t, _replay_text(t)), f)
+    g = ingest_json(str(p))
+    n = 4
+    e = crdt_amd.Engine(n, 32)
+    ag = e.agent_intern(list(range(n)), ["jeremy"] * n)
+    assert (e.apply_trace(list(range(n)), int(ag[0]), g.counts, g.patches) == 0).all()
+    e.set_content(list(range(n)), [0] * n, [content_by_order(g)])
+    for d in range(n):
+        assert utf32_to_str(e.text(d)).encode() == g.end
+    assert (e.lens() == g.end_len).all()
