@@ -153,9 +153,12 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   for (u32 g = 0; g < s.ng; g++) {
     u32 blk = w.root_blk(g), cnt = w.root_cnt(g);
     u32 mydl = P.dir_leaf[(seg.blk_base + blk) * GROUP + l];  // 64-slot row: always in bounds
+    // software pipeline: the next leaf's load is in flight while this leaf is scanned and its
+    // spans stored (vmcnt counts stores too, so an unpipelined load would wait behind them)
+    uint4 vn = cnt ? *(const uint4*)(leaves + (u64)rdlane(mydl, 0) * L + (l & (u32)(L - 1))) : uint4{0, 0, 0, 0};
     for (u32 i = 0; i < cnt; i++) {
-      u32 leaf = rdlane(mydl, i);
-      uint4 v = *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1)));
+      uint4 v = vn;
+      if (i + 1 < cnt) vn = *(const uint4*)(leaves + (u64)rdlane(mydl, i + 1) * L + (l & (u32)(L - 1)));
       bool valid = l < (u32)L && v.w != 0u;  // entries are packed at the front of a leaf
       u32 nn = (u32)__popcll(ballot(valid));
       Span e{v.x, v.y, v.z, (i32)v.w};
