@@ -153,14 +153,34 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   for (u32 g = 0; g < s.ng; g++) {
     u32 blk = w.root_blk(g), cnt = w.root_cnt(g);
     u32 mydl = P.dir_leaf[(seg.blk_base + blk) * GROUP + l];  // 64-slot row: always in bounds
-    // software pipeline: the next leaf's load is in flight while this leaf is scanned and its
-    // spans stored (vmcnt counts stores too, so an unpipelined load would wait behind them)
-    uint4 vn = cnt ? *(const uint4*)(leaves + (u64)rdlane(mydl, 0) * L + (l & (u32)(L - 1))) : uint4{0, 0, 0, 0};
-    for (u32 i = 0; i < cnt; i++) {
+    // 64/L leaves per step: lane l holds entry l%L of leaf i + l/L; the valid entries (packed at
+    // the front of each leaf) are then compacted to lanes [0, nn) with one ds_permute, so the
+    // scan below sees one contiguous run of entries in document order.  Software pipeline: the
+    // next step's loads are in flight while this step is scanned and its spans stored (vmcnt
+    // counts stores too, so an unpipelined load would wait behind them).
+    constexpr u32 PER = 64u / (u32)L;
+    u32 sub = l / (u32)L;
+    auto ld = [&](u32 i) -> uint4 {
+      u32 li = i + sub;
+      u32 leaf = shfl(mydl, li < cnt ? li : 0u);
+      return li < cnt ? *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1))) : uint4{0, 0, 0, 0};
+    };
+    uint4 vn = cnt ? ld(0) : uint4{0, 0, 0, 0};
+    for (u32 i = 0; i < cnt; i += PER) {
       uint4 v = vn;
-      if (i + 1 < cnt) vn = *(const uint4*)(leaves + (u64)rdlane(mydl, i + 1) * L + (l & (u32)(L - 1)));
-      bool valid = l < (u32)L && v.w != 0u;  // entries are packed at the front of a leaf
-      u32 nn = (u32)__popcll(ballot(valid));
+      if (i + PER < cnt) vn = ld(i + PER);
+      u64 VM = ballot(v.w != 0u);
+      u32 nn = (u32)__popcll(VM);
+      if (PER > 1) {
+        u64 below = (1ull << l) - 1ull;
+        u32 dst = v.w != 0u ? (u32)__popcll(VM & below) : nn + (u32)__popcll(~VM & below);
+        int a = (int)(dst << 2);
+        v.x = (u32)__builtin_amdgcn_ds_permute(a, (int)v.x);
+        v.y = (u32)__builtin_amdgcn_ds_permute(a, (int)v.y);
+        v.z = (u32)__builtin_amdgcn_ds_permute(a, (int)v.z);
+        v.w = (u32)__builtin_amdgcn_ds_permute(a, (int)v.w);
+      }
+      bool valid = l < nn;
       Span e{v.x, v.y, v.z, (i32)v.w};
       u32 px = shfl(v.x, l - 1u), py = shfl(v.y, l - 1u), pz = shfl(v.z, l - 1u), pw = shfl(v.w, l - 1u);
       Span prev = l == 0u ? open : Span{px, py, pz, (i32)pw};
