@@ -131,6 +131,7 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
   if (d >= n) return;
   ROOT_LDS;
+  __shared__ u32 s_flag[WAVES_PER_BLOCK][64];
   WaveGPU<L> w = wave_with_root<L>(s_root);
   DocState s = w.ldT(P.st + d);
   DocSeg seg = w.ld_seg(P.seg + d);
@@ -227,8 +228,15 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   // canonical span k contains o (no span contains a delete order).  This saves a fill of
   // 4 B x next_order per document.
   u32* so = O.span_of + seg.map_base;
-  // 64 spans at a time: item j of the chunk finds its span by a 6-step search over the
-  // chunk's length prefix (lane-parallel, no per-lane serial loop over a span's items)
+  // 64 spans at a time, then 64 of their items at a time: item j finds its span m as (spans
+  // starting at or before the window's first item) + (span starts flagged in the window at or
+  // before j).  Span lanes flag their start in a 64-slot LDS row tagged with the window number
+  // (no clearing), item lanes read their slot, one ballot gives the start mask.  Item j of span
+  // m has order base_m + j, base = order - start.
+  u32 (*fl)[64] = s_flag;
+  u32 wv = uni(threadIdx.x >> 6);
+  fl[wv][l] = ~0u;
+  u32 tag = 0;
   u64 h = 0;
   for (u32 k0 = 0; k0 < out; k0 += 64) {
     u32 k = k0 + l;
@@ -237,13 +245,18 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
     if (k < out) h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
     u32 Pi = wave_incl_scan(ln);
     u32 T = rdlane(Pi, 63);
+    u32 st = Pi - ln;            // first item of span k within the chunk
+    u32 base = sp.order - st;
     for (u32 t = 0; t < T; t += 64) {
+      ++tag;
+      if (k < out && st > t && st - t < 64u) fl[wv][st - t] = tag;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      u64 H = ballot(fl[wv][l] == tag);
+      u32 m = (u32)__popcll(ballot(k < out && st <= t)) - 1u + (u32)__popcll(H & ((2ull << l) - 1ull));
+      u32 bm = shfl(base, m);
       u32 j = t + l;
-      u32 m = 0;
-      for (u32 step = 32; step; step >>= 1)
-        if (shfl(Pi, m + step - 1u) <= j) m += step;  // m = lanes whose prefix ends at or before j
-      u32 pm = shfl(Pi, m), lm = shfl(ln, m), om = shfl(sp.order, m);
-      if (j < T) so[om + (j - (pm - lm))] = k0 + m;
+      if (j < T) so[bm + j] = k0 + m;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
   }
   const CwoRun* cwo = P.cwo + seg.cwo_base;
