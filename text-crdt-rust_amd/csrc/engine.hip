@@ -719,19 +719,28 @@ int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t w
   std::vector<StreamNeeds> needs(e->n_docs);
   uniq.reserve(e->n_docs);
   std::vector<u32> first_map;
+  // Authors in order of first appearance: interning that list (get_or_create is idempotent per
+  // name) leaves an AgentTable identical to interning every txn's author in txn order, at a cost
+  // of #names instead of #txns per document.
+  std::vector<u32> authors;
+  {
+    std::vector<char> seen(wv.names.size(), 0);
+    for (const auto& t : wv.txns)
+      if (!seen[t.agent_name]) seen[t.agent_name] = 1, authors.push_back(t.agent_name);
+  }
   for (u64 d = 0; d < e->n_docs; d++) {
     ids[d] = d;
-    WireView w2 = wv;
-    if (names && rename_idx < w2.names.size()) w2.names[rename_idx] = names[d];
+    std::vector<std::string> nm = wv.names;  // only the names differ per document
+    if (names && rename_idx < nm.size()) nm[rename_idx] = names[d];
     AgentTable& at = e->docs[d].agents;
     std::vector<Rec> tmp;
     bool fresh = at.names.empty();
     if (d > 0 && fresh && !uniq.empty()) {
       // intern in txn order (authors create, others look up) exactly as encode_remote does
       AgentTable probe = at;
-      for (const auto& t : w2.txns) probe.get_or_create(w2.names[t.agent_name]);
+      for (u32 a : authors) probe.get_or_create(nm[a]);
       std::vector<u32> m;
-      for (const auto& n : w2.names) m.push_back(probe.lookup(n));
+      for (const auto& n : nm) m.push_back(probe.lookup(n));
       if (m == first_map) {
         at = probe;
         sp[d] = &uniq[0];
@@ -739,6 +748,8 @@ int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t w
         continue;
       }
     }
+    WireView w2 = wv;
+    w2.names = std::move(nm);
     uniq.emplace_back();
     encode_remote(uniq.back(), needs[d], at, w2);
     sp[d] = &uniq.back();
