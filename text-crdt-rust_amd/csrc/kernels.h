@@ -326,9 +326,9 @@ __device__ __forceinline__ u32 text_hash(u32 pos, u32 cp) {
 // One block (MAT_WAVES waves) per document; wave w takes chunks w, w+MAT_WAVES, ... of 64
 // canonical spans (each chunk's output starts at vpos[k0], so chunks are independent).  Within a
 // chunk a prefix scan of the visible lengths gives each output position j; lane l owns positions
-// t+l and finds its span by a 6-step search over the scan (bpermute), so stores are fully
-// coalesced (contiguous positions) and loads are contiguous within a span.  U positions per lane
-// are in flight per step.
+// t+l and finds its span through LDS start flags (below), so stores are fully coalesced
+// (contiguous positions) and loads are contiguous within a span.  U positions per lane are in
+// flight per step.
 #define MAT_WAVES 4
 template <int L>
 __global__ __launch_bounds__(64 * MAT_WAVES) void k_materialize(Pools P, PubOut O, TextIO T, u32 n) {
@@ -351,6 +351,15 @@ __global__ __launch_bounds__(64 * MAT_WAVES) void k_materialize(Pools P, PubOut 
   const u32* src = T.content + cb;
   u32* dst = T.text + seg.map_base;
   constexpr u32 U = 4;
+  // span of output position j: spans with visible items flag their first position in a 64-slot
+  // LDS row per window (tag = step number, no clearing) together with base = order - start;
+  // position j takes the highest flag at or below it, else the last span starting at or before
+  // the window (a uniform readlane).  Two LDS writes, one ballot and one LDS read per window
+  // instead of a 6-step bpermute search.
+  __shared__ u32 s_tag[MAT_WAVES][U][64], s_base[MAT_WAVES][U][64];
+#pragma unroll
+  for (u32 u = 0; u < U; u++) s_tag[wv][u][l] = ~0u;
+  u32 tag = 0;
   u64 h = 0;
   for (u32 k0 = wv * 64; k0 < ns; k0 += 64 * MAT_WAVES) {
     u32 k = k0 + l;
@@ -359,18 +368,32 @@ __global__ __launch_bounds__(64 * MAT_WAVES) void k_materialize(Pools P, PubOut 
     u32 base = uni(vp[k0]);
     u32 Pi = wave_incl_scan(ln);
     u32 Tn = rdlane(Pi, 63);
+    u32 st = Pi - ln;            // first output position of span k within the chunk
+    u32 ob = sp.order - st;      // content index of position j in span k = ob + j
     for (u32 t = 0; t < Tn; t += 64 * U) {
+      ++tag;
+#pragma unroll
+      for (u32 u = 0; u < U; u++) {
+        u32 tu = t + u * 64;
+        if (ln > 0 && st >= tu && st - tu < 64u) {
+          s_tag[wv][u][st - tu] = tag;
+          s_base[wv][u][st - tu] = ob;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       u32 cp[U], jj[U];
 #pragma unroll
       for (u32 u = 0; u < U; u++) {
-        u32 j = t + u * 64 + l;
-        u32 m = 0;
-        for (u32 step = 32; step; step >>= 1)
-          if (shfl(Pi, m + step - 1u) <= j) m += step;  // m = lanes whose prefix ends at or before j
-        u32 pm = shfl(Pi, m), lm = shfl(ln, m), om = shfl(sp.order, m);
+        u32 tu = t + u * 64;
+        u32 j = tu + l;
+        u64 hm = ballot(s_tag[wv][u][l] == tag) & ((2ull << l) - 1ull);
+        u64 B0 = ballot(ln > 0 && st <= tu);
+        u32 lt = B0 ? 63u - (u32)__builtin_clzll(B0) : 0u;
+        u32 b = hm ? s_base[wv][u][63u - (u32)__builtin_clzll(hm)] : rdlane(ob, lt);
         jj[u] = j;
-        cp[u] = j < Tn ? src[om + (j - (pm - lm))] : 0u;
+        cp[u] = j < Tn ? src[b + j] : 0u;
       }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 #pragma unroll
       for (u32 u = 0; u < U; u++) {
         if (jj[u] < Tn) {
