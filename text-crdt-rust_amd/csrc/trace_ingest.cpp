@@ -50,6 +50,22 @@ class Source {
     return c;
   }
   uint64_t offset() const { return consumed_; }
+  // Append the run of plain printable ASCII (no '"' or '\\') at the cursor to `out`, within the
+  // current window; returns its length (one scalar per byte).
+  uint64_t take_ascii(std::string& out) {
+    if (pos_ == n_ && !refill()) return 0;
+    const char* b = cur() + pos_;
+    uint64_t k = 0, lim = n_ - pos_;
+    while (k < lim) {
+      unsigned char c = (unsigned char)b[k];
+      if (c < 0x20 || c >= 0x7F || c == '"' || c == '\\') break;
+      ++k;
+    }
+    out.append(b, k);
+    pos_ += k;
+    consumed_ += k;
+    return k;
+  }
 
  private:
   const char* cur() const { return mem_ ? mem_ : buf_.data(); }
@@ -206,6 +222,7 @@ class Parser {
     if (s_.get() != '"') fail("expected a string");
     uint64_t n = 0;
     for (;;) {
+      n += s_.take_ascii(out);
       int c = s_.get();
       if (c < 0) fail("unterminated string");
       if (c == '"') break;
