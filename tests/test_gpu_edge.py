@@ -115,3 +115,31 @@ def test_tables_grow_during_replay():
     assert st[0] == 0
     assert_same(e.export(0), o.export())
     assert int(e.digests()[0]) == o.digest()
+
+
+def test_republish_after_different_history():
+    # k_publish writes span_of at item orders only; after a reset and a different history, the
+    # entries it leaves at the new history's delete orders are stale and loc->pos must reject them
+    import crdt_amd
+    from crdt_amd.traces import load_trace
+    from oracle_lib import OracleDoc
+    A, B = load_trace("rustcode"), load_trace("sveltecomponent")
+    cA, cB = A.counts[:6000], B.counts[:4000]
+    pA, pB = A.patches[: int(cA.sum())], B.patches[: int(cB.sum())]
+    e = crdt_amd.Engine(2, 32)
+    ag = e.agent_intern([0, 1], ["jeremy"] * 2)
+    assert (e.apply_trace([0, 1], int(ag[0]), cA, pA) == 0).all()
+    nA = int(pA[:, 1].sum() + pA[:, 2].sum())
+    e.loc_to_pos(np.zeros(nA, np.uint32), np.full(nA, ag[0], np.uint16), np.arange(nA, dtype=np.uint32))
+    e.reset_async()
+    assert (e.apply_trace([0, 1], int(ag[0]), cB, pB) == 0).all()
+    o = OracleDoc(32, 16)
+    oa = o.agent("jeremy")
+    assert o.apply_trace(oa, cB, pB) == 0
+    nB = int(pB[:, 1].sum() + pB[:, 2].sum())
+    seqs = np.arange(nB + 64, dtype=np.uint32)
+    op, odl = o.loc_to_pos(np.full(seqs.shape[0], oa, np.uint16), seqs)
+    assert (odl == 2).any() and (odl == 1).any()        # delete-op seqs and deleted items both covered
+    for d in (0, 1):
+        gp, gdl = e.loc_to_pos(np.full(seqs.shape[0], d, np.uint32), np.full(seqs.shape[0], ag[d], np.uint16), seqs)
+        assert np.array_equal(gdl, odl) and np.array_equal(gp, op)
