@@ -5,16 +5,23 @@ Workload (BASELINE config 2): `--docs` (default 4096) independent c
 automerge-paper trace per GPU, delivered as remote txns (apply_remote_txn path) with randomised
 client ids (agent name = hex(splitmix64(0xC0FFEE ^ doc))).  One step = reset all documents to
 ListCRDT::new(), replay every document's 259,778 remote ops (merge: (agent,seq)->order remap +
-integrate + deletes), rebuild the flat position index (publish), and answer one pos->loc and one
-loc->pos query per op position sample.  Inputs are staged in HBM before timing.
+integrate + deletes), rebuild the flat position index (publish), and answer `--queries` pos->loc
+and loc->pos queries per document.  Inputs are staged in HBM before timing.
 
-Multi-GPU: one process per GPU (torchrun); documents shard across ranks with no per-op
-communication; the single collective is an all-gather of per-document digests (RCCL) after the
-timed region.  `value` = total ops of all ranks / max-over-ranks step time.
+Multi-GPU: one process per GPU.  `--gpus N` with N > 1 started by hand spawns the N
+ranks through torch.distributed.run (the parent never touches a GPU); under torchrun the ranks
+read RANK / LOCAL_RANK / WORLD_SIZE.  The global corpus is N x `--docs` documents, sharded into
+contiguous ranges balanced by op count; no per-op communication.  The collectives are the max
+over ranks of the elapsed time, an all-gather of per-rank times and one all-gather of the per-
+document u64 digests (RCCL), all after the timed region.  `value` = total ops of all ranks /
+max-over-ranks time.  `--rehearse-cpu` runs the same launch / shard / collective plumbing on CPU
+ranks over gloo with no GPU (the per-document results are the committed golden digests).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -22,6 +29,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "text-crdt-rust_amd"))
+
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E (MI355X_MICROARCH.md)
+SIMDS = 256 * 4                 # 256 CUs x 4 SIMDs
 
 
 def splitmix64(x):
@@ -37,7 +47,7 @@ def doc_name(d):
 
 
 def wire_ops(w: bytes):
-    """number of RemoteOps and records in a wire batch (ops are what the metric counts)."""
+    """number of RemoteOps, wire records and txns in a wire batch (ops are what the metric counts)."""
     import struct
     off = 8
     nn = struct.unpack_from("<I", w, 4)[0]
@@ -58,59 +68,176 @@ def wire_ops(w: bytes):
     return ops, recs, nt
 
 
-def cpu_baseline(wire: bytes, n_docs: int, threads: int):
-    """The oracle (C++ restatement of the reference B-tree path, leaf 32 / node 16) replaying the
-    same remote workload on host cores, one document per task (rayon-equivalent work queue)."""
+# ------------------------------------------------------------------------------------------------
+# multi-GPU plumbing
+# ------------------------------------------------------------------------------------------------
+def shard_balanced(weights, world: int, rank: int):
+    """Contiguous document range [lo, lo+n) of `rank`, balanced by the documents' weights (op
+    counts): rank r starts at the first document whose weight prefix reaches
+    r/world of the total."""
+    assert 0 <= rank < world
+    w = np.asarray(weights, dtype=np.float64)
+    pre = np.concatenate([[0.0], np.cumsum(w)])
+    cut = [int(np.searchsorted(pre[1:], pre[-1] * r / world, side="right")) if r else 0 for r in range(world + 1)]
+    cut[world] = len(w)
+    for r in range(1, world + 1):
+        cut[r] = max(cut[r], cut[r - 1])
+    return cut[rank], cut[rank + 1] - cut[rank]
+
+
+def shard(rank: int, world: int, docs_per_rank: int):
+    """Weak scaling: the global corpus is world x docs_per_rank documents of equal work (config 2),
+    so the balanced ranges are [r*n, (r+1)*n)."""
+    return shard_balanced(np.ones(world * docs_per_rank), world, rank)
+
+
+def reduce_over_ranks(elapsed: float, digests: np.ndarray, dist, device):
+    """The only collectives: max of the per-rank elapsed time, all-gather of the per-rank times,
+    and one all-gather of the per-document u64 digests (RCCL on the GPU path, gloo in the CPU
+    rehearsal).  Returns (max time, per-rank times, all digests in rank order)."""
+    import torch
+    if dist is None:
+        return elapsed, [elapsed], digests
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    ts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(ts, t)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    # all_gather needs equal sizes: pad each rank's digests to the largest shard
+    n = torch.tensor([len(digests)], device=device, dtype=torch.int64)
+    ns = [torch.empty_like(n) for _ in range(dist.get_world_size())]
+    dist.all_gather(ns, n)
+    m = int(max(int(x.item()) for x in ns))
+    pad = np.zeros(m, np.uint64)
+    pad[:len(digests)] = digests
+    g = torch.from_numpy(pad.view(np.int64)).to(device)
+    outs = [torch.empty_like(g) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, g)
+    alld = np.concatenate([o.cpu().numpy().view(np.uint64)[:int(k.item())] for o, k in zip(outs, ns)])
+    return float(t.item()), [float(x.item()) for x in ts], alld
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started by hand: run N ranks under torch.distributed.run, one process per
+    GPU, and exit with its status.  The parent process never initialises a GPU."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline (the oracle's restatement of the reference's B-tree path; cpu_baseline leg only)
+# ------------------------------------------------------------------------------------------------
+def cpu_share():
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU quota if one is set
+    (a GPU box's share can be far below os.cpu_count())."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    return (min(n, quota) if quota else n), n, quota
+
+
+def cpu_baseline_remote(wire: bytes, n_docs: int, threads: int):
+    """Config 2 on host cores: the oracle (C++ restatement of the reference B-tree path: leaf 32,
+    node 16, SplitList order index with bucket 100) replays the same remote workload, one document
+    per task from an atomic work queue (rayon-equivalent)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
     from oracle_lib import lib as olib
     L = olib()
     names = (C.c_char_p * n_docs)(*[doc_name(d).encode() for d in range(n_docs)])
     ck = C.c_uint64()
-    secs = L.orc_cpu_baseline_remote(n_docs, threads, wire, len(wire), 0xFFFFFFFF, names, C.byref(ck))
-    return secs
+    return L.orc_cpu_baseline_remote(n_docs, threads, wire, len(wire), 0xFFFFFFFF, names, C.byref(ck), 1)
 
 
-def cpu_baseline_sampled(wire: bytes, threads: int, target_s: float, max_docs: int = 16384):
-    """Bounded sample: one calibration pass (one document per thread), then as many documents as
+def cpu_baseline_local(trace, n_docs: int, threads: int):
+    """Config 1's CPU reference path (benches/yjs.rs:41-48: ListCRDT::new + apply_local_txn per
+    txn) on the restatement, `threads` threads, one document per task."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+    from oracle_lib import lib as olib
+    L = olib()
+    c = np.ascontiguousarray(trace.counts, np.uint32)
+    p = np.ascontiguousarray(trace.patches, np.uint32)
+    ck = C.c_uint64()
+    return L.orc_cpu_baseline_local(n_docs, threads, c.shape[0], c.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                    p.ctypes.data_as(C.POINTER(C.c_uint32)), C.byref(ck), 1)
+
+
+def sampled(fn, threads: int, target_s: float, max_docs: int = 16384):
+    """Bounded sample: one calibration pass (four documents per thread), then as many documents as
     fill about `target_s` seconds.  Returns (docs, seconds)."""
-    t_cal = cpu_baseline(wire, 4 * threads, threads)
+    t_cal = fn(4 * threads)
     per_doc = max(t_cal / (4 * threads), 1e-4)
     n = int(min(max_docs, max(threads, target_s / per_doc)))
-    return n, cpu_baseline(wire, n, threads)
+    return n, fn(n)
 
 
-def shard(rank: int, world: int, docs_per_rank: int):
-    """Weak scaling: rank r owns documents [r*n, (r+1)*n) of the global corpus (no
-    per-op communication between ranks)."""
-    assert 0 <= rank < world
-    return rank * docs_per_rank, docs_per_rank
+def cpu_baseline(wire, n_ops_doc, target_s):
+    from crdt_amd.traces import load_trace
+    threads, affinity, quota = cpu_share()
+    cd, secs = sampled(lambda k: cpu_baseline_remote(wire, k, threads), threads, target_s)
+    ap = load_trace("automerge-paper")
+    n1, s1 = sampled(lambda k: cpu_baseline_local(ap, k, 1), 1, max(2.0, target_s / 8), 64)
+    return {"value": n_ops_doc * cd / secs, "unit": "ops/s", "cores": threads, "threads_used": threads,
+            "host_cores": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+            "kind": "port",
+            "sample": f"{cd} docs x automerge-paper remote replay ({n_ops_doc} ops each) on {threads} threads, "
+                      f"one doc per task; {secs:.2f} s.  Oracle C++ restatement of the reference B-tree path "
+                      f"(leaf 32 / node 16, SplitList order index, bucket 100), -O3",
+            "single_thread": {"config": "config1: automerge-paper as local txns (benches/yjs.rs:41-48), 1 thread",
+                              "value": ap.n_patches * n1 / s1, "unit": "ops/s", "docs": n1, "seconds": s1}}
 
 
-def reduce_over_ranks(elapsed: float, digests: np.ndarray, dist, device):
-    """The only collectives: max of the per-rank elapsed time, and one all-gather of the per-
-    document u64 digests (RCCL on the GPU path, gloo in the CPU rehearsal test)."""
-    import torch
-    if dist is None:
-        return elapsed, digests
-    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    g = torch.from_numpy(np.ascontiguousarray(digests).view(np.int64)).to(device)
-    outs = [torch.empty_like(g) for _ in range(dist.get_world_size())]
-    dist.all_gather(outs, g)
-    return float(t.item()), torch.cat(outs).cpu().numpy().view(np.uint64)
+# ------------------------------------------------------------------------------------------------
+# measurement helpers
+# ------------------------------------------------------------------------------------------------
+def golden(trace: str, key: str):
+    """Committed fixture (tests/golden/oracle_golden.json) of the oracle's replay of the trace."""
+    p = os.path.join(ROOT, "tests", "golden", "oracle_golden.json")
+    try:
+        return json.load(open(p))[f"{trace}/L32"][key]
+    except (OSError, KeyError):
+        return None
+
+
+def measured_traffic(n_docs: int, kernel: str = "k_replay"):
+    """HBM bytes per launch of `kernel` from the committed PMC pass (profiles/traffic_<kernel>.json:
+    FETCH_SIZE x 2 + WRITE_SIZE per the MI355X guide's gfx950 correction), scaled per document."""
+    p = os.path.join(ROOT, "profiles", f"traffic_{kernel}.json")
+    try:
+        t = json.load(open(p))
+        return t["hbm_bytes_per_launch"] / t["docs"] * n_docs
+    except (OSError, KeyError, ZeroDivisionError):
+        return None
 
 
 def materialize_leg(eng, trace, n, hip, ev, s_, reps=5):
-    """Text materialisation, measured outside the timed step: every document
-    shares the trace's order-indexed content stream; k_materialize writes each document's text
-    from the published index.  Algorithmic bytes per document: canonical spans read (16 B) + vpos
-    read (4 B) per span, content read (4 B) + text written (4 B) per visible char.  Parity: every
-    document's text digest == the committed golden text digest (== the trace's endContent)."""
+    """Text materialisation, measured outside the timed step.  Every document
+    reads its own copy of the trace's order-indexed content (a per-document stream, so the
+    content reads come from HBM, not from a shared cache-resident stream); k_materialize writes
+    each document's text from the published index.  Algorithmic bytes per document: canonical
+    spans read (16 B) + vpos read (4 B) per span, content read (4 B) + text written (4 B) per
+    visible char.  Parity: every document's text digest == the committed golden text digest
+    (== the trace's endContent)."""
     import ctypes as C
-    import json
     from crdt_amd.traces import content_by_order, load_trace
-    eng.set_content(list(range(n)), [0] * n, [content_by_order(load_trace(trace))])
+    c = content_by_order(load_trace(trace))
+    eng.set_content_copies(list(range(n)), c)
     eng.materialize_async()
     eng.sync()
     ms = []
@@ -123,47 +250,39 @@ def materialize_leg(eng, trace, n, hip, ev, s_, reps=5):
         hip.hipEventElapsedTime(C.byref(x), ev[2], ev[3])
         ms.append(x.value)
     tdg = eng.text_digests()
-    e0 = eng.export(0)
+    canon_n = eng.export_sizes(0)["canon"]
     lens = eng.lens()
-    canon_n = e0["canon"].shape[0]
     alg = int(n * canon_n * 20 + int(lens.astype(np.int64).sum()) * 8)
     k_ms = float(np.mean(ms))
-    gold = None
-    try:
-        gold = int(json.load(open(os.path.join(ROOT, "tests", "golden", "oracle_golden.json")))[f"{trace}/L32"]["text_digest"], 16)
-    except (OSError, KeyError):
-        pass
+    gold = golden(trace, "text_digest")
+    eng.set_content_copies([], c[:0])  # release the per-document content copies
     return {"kernel": "k_materialize<32>", "kernel_ms": k_ms, "chars_per_s": float(lens.sum()) / (k_ms * 1e-3),
-            "roofline": {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                         "frac": alg / (k_ms * 1e-3) / 1e9 / 8000.0, "alg_bytes_per_launch": alg,
+            "content": "one order-indexed content copy per document",
+            "roofline": {"bound": "hbm", "achieved": alg / (k_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / (k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "alg_bytes_per_launch": alg,
                          "traffic": measured_traffic(n, "k_materialize")},
-            "parity_ok": bool(gold is not None and (tdg == np.uint64(gold)).all()),
+            "parity_ok": bool(gold is not None and (tdg == np.uint64(int(gold, 16))).all()),
             "parity": "every document's text digest == committed golden text digest (== endContent FNV, tests/golden)"}
 
 
-def golden_digest(trace: str):
-    """Committed fixture (tests/golden/oracle_golden.json): the oracle's digest of the trace's
-    remote replay with the release layout.  Every document of the bench must reproduce it."""
-    import json
-    p = os.path.join(ROOT, "tests", "golden", "oracle_golden.json")
-    try:
-        return int(json.load(open(p))[f"{trace}/L32"]["remote_digest"], 16)
-    except (OSError, KeyError):
-        return None
+def rehearse_cpu(args, world, rank, dist):
+    """--rehearse-cpu: launch, shard and collectives exactly as on the GPU path, on CPU ranks over
+    gloo; each document's 'result' is the committed golden digest (no engine, no GPU)."""
+    import torch
+    doc0, n = shard(rank, world, args.docs)
+    gold = int(golden(args.trace, "remote_digest"), 16)
+    dg = np.full(n, gold, np.uint64)
+    t0 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
+    t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"rehearsal": "cpu-gloo", "n_gpus": world, "world_size": dist.get_world_size() if dist else 1,
+                          "docs_total": int(all_dg.shape[0]), "shards": [list(shard(r, world, args.docs)) for r in range(world)],
+                          "per_rank_s": per_rank, "parity_ok": bool((all_dg == np.uint64(gold)).all()),
+                          "value": None}))
 
 
-def measured_traffic(n_docs: int, kernel: str = "k_replay"):
-    """HBM bytes per launch of `kernel` from the committed PMC pass (profiles/traffic_<kernel>.json:
-    FETCH_SIZE x 2 + WRITE_SIZE per the MI355X guide's gfx950 correction), scaled per document."""
-    import json
-    p = os.path.join(ROOT, "profiles", f"traffic_{kernel}.json")
-    try:
-        t = json.load(open(p))
-        return t["hbm_bytes_per_launch"] / t["docs"] * n_docs
-    except (OSError, KeyError, ZeroDivisionError):
-        return None
-
-
+# ------------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,18 +294,34 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-text", action="store_true", help="skip the text materialisation leg")
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
+    ap.add_argument("--rehearse-cpu", action="store_true", help="CPU/gloo rehearsal of the multi-rank plumbing")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+        sys.exit(2)
+    import torch
     dist = None
+    if args.rehearse_cpu:
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+        rehearse_cpu(args, world, rank, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    if torch.cuda.device_count() < (world if world > 1 else 1):  # (counting devices does not initialise them)
+        print(f"bench.py: {world} rank(s) need {world} GPU(s); {torch.cuda.device_count()} visible", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
-        import torch
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl")
-    import torch
     import crdt_amd
     from crdt_amd.traces import load_remote_wire
 
@@ -219,20 +354,20 @@ def main():
     torch.cuda.synchronize()
     L = eng.L
 
-    def step():
-        eng.reset_async()
-        eng.run_async()
-        eng.publish_async()
+    def queries():
         if q:
             L.crdt_pos_to_loc_dev_async(eng.h, n * q, d_doc.data_ptr(), d_pos.data_ptr(), d_ag.data_ptr(), d_seq.data_ptr())
             L.crdt_loc_to_pos_dev_async(eng.h, n * q, d_doc.data_ptr(), d_ag.data_ptr(), d_seq.data_ptr(),
                                         d_p2.data_ptr(), d_del.data_ptr())
 
     for _ in range(args.warmup):
-        step()
+        eng.reset_async()
+        eng.run_async()
+        eng.publish_async()
+        queries()
     eng.sync()
     torch.cuda.synchronize()
-    # HIP events on the engine stream around the replay kernel (dominant kernel)
+    # HIP events on the engine stream around the replay kernel (the dominant kernel)
     import ctypes as C
     hip = C.CDLL("libamdhip64.so")
     ev = [C.c_void_p() for _ in range(4)]
@@ -250,10 +385,7 @@ def main():
         eng.run_async()
         hip.hipEventRecord(ev[1], s_)
         eng.publish_async()
-        if q:
-            L.crdt_pos_to_loc_dev_async(eng.h, n * q, d_doc.data_ptr(), d_pos.data_ptr(), d_ag.data_ptr(), d_seq.data_ptr())
-            L.crdt_loc_to_pos_dev_async(eng.h, n * q, d_doc.data_ptr(), d_ag.data_ptr(), d_seq.data_ptr(),
-                                        d_p2.data_ptr(), d_del.data_ptr())
+        queries()
         hip.hipEventSynchronize(ev[1])
         ms = C.c_float()
         hip.hipEventElapsedTime(C.byref(ms), ev[0], ev[1])
@@ -263,34 +395,32 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    # parity: every document's state digest == the committed oracle digest, and every timed query
+    # answer round-trips (loc_to_pos(pos_to_loc(p)) == p, visible, by the document's only author)
     st = eng.status()
     ok = bool((st == 0).all())
+    q_ok = bool(((d_p2 == d_pos) & (d_del == 0) & (d_ag == 0)).all().item()) if q else True
     dg = eng.digests()
-    t_max, all_dg = reduce_over_ranks(elapsed, dg, dist, dev)
-    gold = golden_digest(args.trace)
-    ok = ok and bool((all_dg == all_dg[0]).all()) and (gold is None or int(all_dg[0]) == gold)
+    t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, dev)
+    gold = golden(args.trace, "remote_digest")
+    gold = int(gold, 16) if gold else None
+    ok = ok and q_ok and bool((all_dg == all_dg[0]).all()) and (gold is None or int(all_dg[0]) == gold)
     mat = materialize_leg(eng, args.trace, n, hip, ev, s_) if not args.no_text else None
-    total_ops = n_ops_doc * n * world * args.steps
+    total_ops = n_ops_doc * int(all_dg.shape[0]) * args.steps
     value = total_ops / t_max
     ms_step = t_max / args.steps * 1e3
     rms = float(np.mean(replay_ms)) if replay_ms else None
-    # algorithmic bytes of one replay launch: every record read once (16 B) + the final per-doc
-    # state written once (entries 16 B, directory 8 B/slot, order->leaf 4 B/order, RLE tables).
-    e0 = eng.export(0)
-    state_bytes = e0["raw"].shape[0] * 16 + e0["leaf_sizes"].shape[0] * (8 + 4) + e0["next_order"] * 4 + \
-        e0["deletes"].shape[0] * 12 + e0["cwo"].shape[0] * 16 + e0["txns"].shape[0] * 32
-    alg_bytes = n * (n_recs_doc * 16 + state_bytes)
+    # roofline of k_replay, SURVEY §8(d) algorithmic bytes for one launch = the whole trace per
+    # document, starting from empty documents (S = 0): 32 B per final canonical span (16 B span
+    # written + 8 B vpos/rpos + 8 B order->span) + 24 B per op (16 B op in + 8 B result out)
+    sz = eng.export_sizes(0)
+    canon = sz["canon"]
+    alg_bytes = n * (32 * canon + 24 * n_ops_doc)
     achieved = alg_bytes / (rms * 1e-3) / 1e9 if rms else None
+    enc_bytes = n * (n_recs_doc * 16 + sz["raw"] * 16 + sz["leaves"] * 12 + sz["next_order"] * 4)
     out = None
     if rank == 0:
-        cpu = None
-        if not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)
-            cd, secs = cpu_baseline_sampled(wire, threads, args.cpu_seconds)
-            cpu = {"value": n_ops_doc * cd / secs, "unit": "ops/s", "cores": threads, "kind": "port",
-                   "sample": f"{cd} docs x {args.trace} remote replay ({n_ops_doc} ops each), oracle C++ "
-                             f"restatement of the reference B-tree path (leaf 32/node 16), {threads} threads, "
-                             f"one doc per task; {secs:.2f} s"}
+        cpu = cpu_baseline(wire, n_ops_doc, args.cpu_seconds) if not args.no_cpu else None
         out = {
             "metric": "CRDT ops remapped+merged/sec (whole node)",
             "value": value,
@@ -306,14 +436,22 @@ def main():
             "data": "synthetic-from-trace: benchmark_data/automerge-paper remote form, randomised client ids",
             "config": {"workload": f"config2: {n} docs/GPU x {args.trace} remote txns ({n_ops_doc} ops/doc), "
                                    f"replay+publish+{q} pos->loc & loc->pos queries/doc",
-                       "docs_per_gpu": n, "ops_per_doc": n_ops_doc, "parallelism": f"doc-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": (achieved / 8000.0) if achieved else None, "traffic": measured_traffic(n),
-                         "kernel": "k_replay<32>", "kernel_ms": rms,
-                         "alg_bytes_per_launch": alg_bytes},
+                       "docs_per_gpu": n, "ops_per_doc": n_ops_doc, "parallelism": f"doc-sharded x{world}",
+                       "waves_per_simd": n / SIMDS},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": measured_traffic(n),
+                         "kernel": "k_replay<32>", "kernel_ms": rms, "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops)",
+                         "canonical_spans_per_doc": canon,
+                         "encoding_bytes_per_launch": enc_bytes,
+                         "encoding_bytes_note": "the engine's own record stream + final raw state (not algorithmic)"},
             "cpu_baseline": cpu,
             "parity_ok": ok,
-            "parity": "every document's digest == committed oracle golden digest (tests/golden)",
+            "parity": "every document's digest == committed oracle golden digest (tests/golden); every timed "
+                      "pos->loc answer round-trips through loc->pos",
+            "queries_ok": q_ok,
+            "world_size": dist.get_world_size() if dist is not None else 1,
+            "per_rank_ops_s": [n_ops_doc * n * args.steps / t for t in per_rank],
             "stage_s": stage_s,
             "materialize": mat,
         }

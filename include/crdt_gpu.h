@@ -154,6 +154,10 @@ int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
 int crdt_set_content(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* stream_of_doc,
                      uint32_t n_streams, const uint64_t* stream_off, const uint32_t* content);
 /* Write every document's text on the device (publishes first if needed; stream-ordered). */
+// As crdt_set_content, with one stream that every listed document gets its own device copy of
+// (docs[i] reads copy i); replaces all previously set content.
+int crdt_set_content_copies(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* content,
+                            uint64_t len);
 int crdt_materialize_async(crdt_engine* e);
 /* ListCRDT::to_string (doc.rs:498-505) as UTF-32: *n_out = visible chars; out may be NULL (size
  * query), else cap >= *n_out.  CRDT_E_ARG if the document has no content or its stream is shorter
@@ -180,7 +184,7 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
                 uint32_t* frontier);
 
 /* Raw per-document replay state (22 u32: status, resume point, table sizes, ...; debugging). */
-int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out22);
+int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23);
 /* Device time of the last replay / publish launches in ms (HIP events on the engine stream). */
 int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms);
 /* Engine stream (hipStream_t) for callers that time or order their own work. */

@@ -540,19 +540,140 @@ struct Tree {
   }
 };
 
-// order -> leaf.  Semantically the reference's SplitList (split_list/mod.rs) restricted to what
-// ListCRDT reads: marker_at(order) for item orders (doc.rs:101-107).  Stored as an interval map;
-// replace_range == SplitList::replace_range (:235-336).
+// The reference's SplitList (split_list/mod.rs) of MarkerEntry{len, ptr} (list/markers.rs:7-89),
+// restated step for step: buckets of 100 orders (:12), each an RLE list of markers; `can_append`
+// = same leaf pointer.  This is the order index the CPU baseline times (the reference algorithm).
+struct SplitListIndex {
+  static constexpr size_t B = 100;   // DEFAULT_BUCKET_SIZE (split_list/mod.rs:12)
+  struct Marker { u32 len; Leaf* ptr; };
+  std::vector<std::vector<Marker>> content;
+  size_t total_len = 0;
+  // get_internal_idx (:95-136): (bucket, offset in bucket, cursor idx, cursor offset)
+  void internal_idx(size_t index, bool stick_end, size_t& bi, size_t& boff, size_t& ci, size_t& co) const {
+    ci = 0;
+    co = 0;
+    bi = index / B;
+    boff = index - bi * B;
+    if (boff == 0) return;  // (index 0 included) may point past the end of the list
+    size_t off = boff;
+    const auto& b = content[bi];
+    for (size_t i = 0; i < b.size(); i++) {
+      size_t len = b[i].len;
+      if (off < len || (stick_end && off == len)) { ci = i; co = off; return; }
+      off -= len;
+    }
+  }
+  // slice_insert (:174-218).  Returns true with the displaced remainder in `rem`.
+  static bool slice_insert(std::vector<Marker>& b, Marker e, size_t& ci, size_t& co, Marker& rem) {
+    if (co == 0) {
+      co = e.len;
+      b.insert(b.begin() + ci, e);
+      return false;
+    }
+    Marker& item = b[ci];
+    bool has_rem = false;
+    if (co != item.len) {  // item.truncate(offset)
+      rem = Marker{item.len - (u32)co, item.ptr};
+      item.len = (u32)co;
+      has_rem = true;
+    }
+    if (item.ptr == e.ptr) {  // can_append + append
+      co += e.len;
+      item.len += e.len;
+    } else {
+      ci += 1;
+      co = e.len;
+      if (ci < b.size() && e.ptr == b[ci].ptr) {  // prepend onto the next entry
+        b[ci].len += e.len;
+        return has_rem;
+      }
+      b.insert(b.begin() + ci, e);
+    }
+    return has_rem;
+  }
+  static void insert_at(std::vector<Marker>& b, Marker e, size_t& ci, size_t& co) {  // :221-232
+    Marker rem;
+    while (slice_insert(b, e, ci, co, rem)) e = rem;
+  }
+  // replace_range (:235-336)
+  void replace_range(size_t index, Marker entry) {
+    size_t bi, boff, ci, co;
+    internal_idx(index, true, bi, boff, ci, co);
+    size_t new_len = entry.len, remaining = new_len;
+    size_t room = B - boff;
+    while (true) {
+      if (bi == content.size()) content.emplace_back();  // appending to the end of the list
+      bool spill = false;
+      Marker next_rem{0, nullptr};
+      size_t here;
+      if (room >= remaining) here = remaining;
+      else {  // entry.truncate(room): the rest goes to the next bucket
+        next_rem = Marker{entry.len - (u32)room, entry.ptr};
+        entry.len = (u32)room;
+        spill = true;
+        here = room;
+      }
+      auto& b = content[bi];
+      Marker rem;
+      if (slice_insert(b, entry, ci, co, rem)) {
+        if (rem.len > here) {  // discard the start of the remainder, re-insert the rest
+          insert_at(b, Marker{rem.len - (u32)here, rem.ptr}, ci, co);
+          break;
+        }
+        here -= rem.len;
+      }
+      while (here > 0) {  // discard / truncate what the entry replaced
+        if (ci < b.size() && co == b[ci].len) { ci++; co = 0; }  // roll_next
+        if (ci >= b.size()) break;
+        size_t hl = b[ci].len;
+        if (here >= hl) { b.erase(b.begin() + ci); here -= hl; }
+        else { b[ci].len = (u32)(hl - here); break; }
+      }
+      if (!spill) break;
+      entry = next_rem;
+      remaining -= room;
+      room = B;
+      bi++;
+      ci = 0;
+      co = 0;
+    }
+    total_len = std::max(total_len, index + new_len);
+  }
+  void append_entry(Marker m) { replace_range(total_len, m); }  // :339-341
+  const Marker* last() const { return content.empty() || content.back().empty() ? nullptr : &content.back().back(); }
+  Leaf* entry_at(size_t index) const {  // :440-443
+    if (index >= total_len) return nullptr;
+    size_t bi, boff, ci, co;
+    internal_idx(index, false, bi, boff, ci, co);
+    if (bi >= content.size() || ci >= content[bi].size()) return nullptr;
+    return content[bi][ci].ptr;
+  }
+};
+
+// order -> leaf: ListCRDT::marker_at (doc.rs:101-107) over either the reference's SplitList
+// (`split`, what the CPU baseline times) or a dense table (faster; identical answers for item
+// orders, which are all ListCRDT reads: delete orders name no item either way).
 struct OrderIndex {
-  // Dense order -> leaf table; replace_range writes the notified run.  Orders that were never
-  // notified (delete orders) stay nullptr.
-  std::vector<Leaf*> v;
-  void replace_range(u32 start, u32 len, Leaf* leaf) {
+  bool split = false;
+  std::vector<Leaf*> v;   // dense: order -> leaf, nullptr for delete orders
+  SplitListIndex sl;
+  void replace_range(u32 start, u32 len, Leaf* leaf) {  // ListCRDT::notify (doc.rs:143-153)
     if (len == 0) return;
+    if (split) { sl.replace_range(start, SplitListIndex::Marker{len, leaf}); return; }
     if ((size_t)start + len > v.size()) v.resize(std::max<size_t>((size_t)start + len, v.size() * 2), nullptr);
     std::fill(v.begin() + start, v.begin() + start + len, leaf);
   }
-  Leaf* at(u32 order) const { return order < v.size() ? v[order] : nullptr; }
+  // doc.rs:337-339 / 402-404: the SplitList cannot hold gaps, so delete orders are padded with
+  // the last marker's leaf
+  void pad(u32 len) {
+    if (!split || len == 0) return;
+    const SplitListIndex::Marker* m = sl.last();
+    sl.append_entry(SplitListIndex::Marker{len, m ? m->ptr : nullptr});
+  }
+  Leaf* at(u32 order) const {
+    if (split) return sl.entry_at(order);
+    return order < v.size() ? v[order] : nullptr;
+  }
 };
 
 inline void Tree::notify(const Span& e, Leaf* leaf) {
@@ -656,9 +777,10 @@ struct Doc {
   int status = OK;
   Stats stats;
 
-  Doc(u32 L = 32, u32 NC = 16, bool track_index = true) : tree(L, NC) {
+  Doc(u32 L = 32, u32 NC = 16, bool track_index = true, bool split_index = false) : tree(L, NC) {
     tree.index = &index;
     tree.track_index = track_index;
+    index.split = split_index;
   }
 
   // doc.rs:66-89
@@ -840,6 +962,7 @@ struct Doc {
           next += (u32)it.len;
         }
         if (dl != ops[i].del) return status = ERR_POS_OOB;
+        if (tree.track_index) index.pad(ops[i].del);
       }
       if (ops[i].ins > 0) {
         u32 order = next;
@@ -911,6 +1034,7 @@ struct Doc {
           remaining -= here;
           target += here;
         }
+        if (tree.track_index) index.pad(op.len);
       }
     }
     std::vector<u32> parents;

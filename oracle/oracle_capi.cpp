@@ -101,7 +101,7 @@ extern "C" {
 
 void* orc_doc_new(uint32_t leaf_cap, uint32_t node_cap, int track_index) {
   if (leaf_cap < 4 || leaf_cap > 32 || node_cap < 8 || node_cap > 16) return nullptr;
-  return new Doc(leaf_cap, node_cap, track_index != 0);
+  return new Doc(leaf_cap, node_cap, track_index != 0, track_index == 2);  // 2: the SplitList index
 }
 void orc_doc_free(void* h) { delete (Doc*)h; }
 int orc_status(void* h) { return ((Doc*)h)->status; }
@@ -283,7 +283,7 @@ uint32_t orc_dd_get(void* h, uint32_t* out3, uint32_t cap) {
 // (rayon-equivalent), `threads` host threads.  Returns seconds of the timed region.
 // ---------------------------------------------------------------------------------------------
 double orc_cpu_baseline_local(uint32_t ndocs, uint32_t threads, uint32_t ntxn, const uint32_t* counts,
-                              const uint32_t* patches3, uint64_t* checksum) {
+                              const uint32_t* patches3, uint64_t* checksum, int split_index) {
   std::atomic<uint32_t> next{0};
   std::atomic<uint64_t> sum{0};
   auto worker = [&]() {
@@ -291,7 +291,7 @@ double orc_cpu_baseline_local(uint32_t ndocs, uint32_t threads, uint32_t ntxn, c
     while (true) {
       uint32_t i = next.fetch_add(1);
       if (i >= ndocs) break;
-      Doc d(32, 16, true);
+      Doc d(32, 16, true, split_index != 0);
       u16 a = d.get_or_create_agent_id("jeremy");
       const LocalOp* p = (const LocalOp*)patches3;
       for (uint32_t t = 0; t < ntxn; t++) { d.apply_local_txn(a, p, counts[t]); p += counts[t]; }
@@ -313,7 +313,7 @@ double orc_cpu_baseline_local(uint32_t ndocs, uint32_t threads, uint32_t ntxn, c
 // index `rename_idx` replaced by names[i] for the first document it owns; names never change the
 // amount of work of a single-agent trace).  Timed region: from a start barrier to the last join.
 double orc_cpu_baseline_remote(uint32_t ndocs, uint32_t threads, const uint8_t* buf, size_t len,
-                               uint32_t rename_idx, const char* const* names, uint64_t* checksum) {
+                               uint32_t rename_idx, const char* const* names, uint64_t* checksum, int split_index) {
   wire::Batch b;
   if (!wire::parse(buf, len, b)) return -1.0;
   std::atomic<uint32_t> next{0}, ready{0};
@@ -331,7 +331,7 @@ double orc_cpu_baseline_remote(uint32_t ndocs, uint32_t threads, const uint8_t* 
     while (true) {
       uint32_t i = next.fetch_add(1);
       if (i >= ndocs) break;
-      Doc d(32, 16, true);
+      Doc d(32, 16, true, split_index != 0);
       for (const auto& t : txns) d.apply_remote_txn(t);
       local += d.len() + (uint64_t)d.status;
     }

@@ -23,6 +23,7 @@ struct EmuDoc {
   std::vector<ARun> arun;
   std::vector<DelRun> dels;
   std::vector<DDRun> dd;
+  std::vector<DDBlk> ddb;
   std::vector<TxnRec> txns;
   std::vector<AgentRec> agent_tab;
   std::vector<GroupRec> groups;
@@ -42,6 +43,7 @@ struct EmuDoc {
     p.arun = arun.data();
     p.dels = dels.data();
     p.dd = dd.data();
+    p.ddb = ddb.data();
     p.txns = txns.data();
     p.parents = parents.data();
     p.frontier = frontier.data();
@@ -64,11 +66,12 @@ struct EmuDoc {
     cwo.assign(c.cwo, CwoRun{});
     arun.assign(c.arun, ARun{});
     dels.assign(c.del, DelRun{});
-    dd.assign(c.dd, DDRun{});
+    dd.assign((size_t)std::max<u32>(c.dd, 1) * DD_BLK, DDRun{});
+    ddb.assign(std::max<u32>(c.dd, 1), DDBlk{});
     txns.assign(c.txn, TxnRec{});
     parents.assign(c.par, 0);
-    frontier.assign(FRONTIER_CAP, 0);
-    groups.assign(MAX_GROUPS, GroupRec{});
+    frontier.assign(c.fr, 0);
+    groups.assign(c.blk, GroupRec{});
     agent_tab.assign(std::max<u32>(c.agent, 1), AgentRec{});
     std::vector<u32> rk = agents.ranks();
     u32 base = 0;
@@ -81,6 +84,7 @@ struct EmuDoc {
     seg.leaf_cap = c.leaf; seg.blk_cap = c.blk; seg.map_cap = c.map; seg.cwo_cap = c.cwo;
     seg.arun_cap = c.arun; seg.del_cap = c.del; seg.dd_cap = c.dd; seg.txn_cap = c.txn;
     seg.par_cap = c.par; seg.agent_cap = c.agent; seg.rec_n = (u32)recs.size();
+    seg.fr_cap = c.fr; seg.grp_cap = c.blk;
     seg.flags = track ? DOC_TRACK_MAP : 0;
     st = DocState{};
     st.n_agents = (u32)agents.names.size();
@@ -97,15 +101,18 @@ struct EmuDoc {
       leaves.resize((size_t)nl * L, Span{0, 0, 0, 0});
       sol.resize(nl, 0);
       seg.leaf_cap = nl;
-      seg.blk_cap = nl / 32 + 2;
+      seg.blk_cap = blk_cap_for(nl);
+      seg.grp_cap = seg.blk_cap;
       dir_leaf.resize((size_t)seg.blk_cap * GROUP, 0);
       dir_vis.resize((size_t)seg.blk_cap * GROUP, 0);
+      groups.resize(seg.grp_cap, GroupRec{});
     }
+    if (need & 128u) { seg.fr_cap *= 2; frontier.resize(seg.fr_cap, 0); }
     if (need & 2u) { seg.cwo_cap *= 2; seg.txn_cap *= 2; cwo.resize(seg.cwo_cap); txns.resize(seg.txn_cap); }
     if (need & 4u) { seg.del_cap = seg.del_cap * 2 + 16; dels.resize(seg.del_cap); }
     if (need & 8u) { seg.par_cap = seg.par_cap * 2 + 16; parents.resize(seg.par_cap); }
     if (need & 16u) { seg.map_cap = seg.map_cap * 2 + 16; leaf_of.resize(seg.map_cap, 0xDEADBEEFu); }
-    if (need & 64u) { seg.dd_cap = seg.dd_cap * 2 + 64; dd.resize(seg.dd_cap); }
+    if (need & 64u) { seg.dd_cap = seg.dd_cap * 2 + 2; dd.resize((size_t)seg.dd_cap * DD_BLK); ddb.resize(seg.dd_cap); }
     if (need & 32u) {  // re-space every agent's run list with doubled capacity
       std::vector<ARun> na;
       for (u32 a = 0; a < st.n_agents; a++) {
@@ -221,7 +228,8 @@ void emu_export(void* h, uint32_t* raw4, uint32_t* leaf_sizes, uint32_t* cwo4, u
   std::memcpy(leaf_sizes, ls.data(), ls.size() * 4);
   std::memcpy(cwo4, d->cwo.data(), d->st.n_cwo * 16);
   std::memcpy(del3, d->dels.data(), d->st.n_del * 12);
-  std::memcpy(dd3, d->dd.data(), d->st.n_dd * 12);
+  for (u32 lb = 0, k = 0; lb < d->st.n_ddb; lb++)
+    for (u32 i = 0; i < d->ddb[lb].cnt; i++, k++) std::memcpy(dd3 + 3 * k, &d->dd[(size_t)d->ddb[lb].phys * DD_BLK + i], 12);
   for (u32 i = 0; i < d->st.n_txn; i++) {
     const TxnRec& t = d->txns[i];
     txn5[5 * i] = t.order; txn5[5 * i + 1] = t.len; txn5[5 * i + 2] = t.shadow; txn5[5 * i + 3] = t.poff; txn5[5 * i + 4] = t.pn;

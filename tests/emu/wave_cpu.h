@@ -12,7 +12,7 @@ namespace crdt {
 template <int L>
 struct WaveCPU {
   Span c[64];
-  u32 gb[MAX_GROUPS], gc[MAX_GROUPS], gv[MAX_GROUPS];
+  u32 gb[ROOT_CAP_MAX], gc[ROOT_CAP_MAX], gv[ROOT_CAP_MAX];
 
   WaveCPU() { std::memset(c, 0, sizeof(c)); std::memset(gb, 0, sizeof(gb)); std::memset(gc, 0, sizeof(gc)); std::memset(gv, 0, sizeof(gv)); }
 
@@ -68,7 +68,23 @@ struct WaveCPU {
   }
   i32 search_arun(const ARun* b, u32 n, u32 x) const { return search(b, n, x); }
   i32 search_cwo(const CwoRun* b, u32 n, u32 x) const { return search(b, n, x); }
-  i32 search_dd(const DDRun* b, u32 n, u32 x) const { return search(b, n, x); }
+  DDBlk ld_ddblk(const DDBlk* p) const { return *p; }
+  void st_ddblk(DDBlk* p, const DDBlk& v) const { *p = v; }
+  i32 search_first(const DDBlk* b, u32 n, u32 x) const {
+    i32 r = -1;
+    for (u32 i = 0; i < n; i++) if (b[i].first <= x) r = (i32)i;
+    return r;
+  }
+  u32 dd_count_le(const DDRun* blk, u32 cnt, u32 x) const { u32 k = 0; for (u32 i = 0; i < cnt; i++) k += blk[i].key <= x; return k; }
+  u32 dd_split(const DDRun* src, DDRun* dst) const { for (u32 i = 32; i < 64; i++) dst[i - 32] = src[i]; return dst[0].key; }
+  void dd_block_insert(DDRun* blk, u32 cnt, u32 i, const DDRun& r) const {
+    for (u32 k = cnt; k > i; k--) blk[k] = blk[k - 1];
+    blk[i] = r;
+  }
+  void ddb_insert(DDBlk* b, u32 n, u32 at, const DDBlk& v) const {
+    for (u32 k = n; k > at; k--) b[k] = b[k - 1];
+    b[at] = v;
+  }
   i32 search_txn(const TxnRec* b, u32 n, u32 x) const { return search(b, n, x); }
 
   // leaf cache

@@ -60,9 +60,9 @@ def lib():
     L.orc_dd_increment.argtypes = [vp, u32, u32]
     L.orc_dd_get.argtypes = [vp, P(u32), u32]
     L.orc_dd_get.restype = u32
-    L.orc_cpu_baseline_local.argtypes = [u32, u32, u32, P(u32), P(u32), P(u64)]
+    L.orc_cpu_baseline_local.argtypes = [u32, u32, u32, P(u32), P(u32), P(u64), C.c_int]
     L.orc_cpu_baseline_local.restype = C.c_double
-    L.orc_cpu_baseline_remote.argtypes = [u32, u32, C.c_char_p, C.c_size_t, u32, P(C.c_char_p), P(u64)]
+    L.orc_cpu_baseline_remote.argtypes = [u32, u32, C.c_char_p, C.c_size_t, u32, P(C.c_char_p), P(u64), C.c_int]
     L.orc_cpu_baseline_remote.restype = C.c_double
     _lib = L
     return L
@@ -75,9 +75,11 @@ def _p(a, t=C.c_uint32):
 class OracleDoc:
     """One reference ListCRDT (restated).  leaf_cap/node_cap: 32/16 release, 4/8 debug."""
 
-    def __init__(self, leaf_cap: int = 32, node_cap: int = 16, track_index: bool = True):
+    def __init__(self, leaf_cap: int = 32, node_cap: int = 16, track_index: bool = True, split_index: bool = False):
+        """split_index: the order index is the reference's SplitList (bucket 100) instead of a dense
+        table (same answers; the CPU baseline uses it)."""
         self.L = lib()
-        self.h = self.L.orc_doc_new(leaf_cap, node_cap, int(track_index))
+        self.h = self.L.orc_doc_new(leaf_cap, node_cap, 2 if (track_index and split_index) else int(track_index))
         if not self.h:
             raise ValueError("bad caps")
 

@@ -12,8 +12,6 @@ from fuzz_gen import random_local_trace, concurrent_wire
 @pytest.mark.parametrize("name", ["sveltecomponent", "rustcode", "automerge-paper"])
 @pytest.mark.parametrize("L", [32, 4])
 def test_traces(name, L):
-    if name == "automerge-paper" and L == 4:
-        pytest.skip("debug layout of automerge-paper needs 25,855 leaves > root capacity (8,160)")
     t = load_trace(name)
     o = OracleDoc(L, 16 if L == 32 else 8)
     o.apply_trace(o.agent("jeremy"), t.counts, t.patches)
@@ -79,3 +77,36 @@ def test_concurrent_config5(seed):
         assert e.run_wire(w, 48) == 0
         assert e.check() == ""
         assert diff_states(o.export(), e.export()) == []
+
+
+@pytest.mark.parametrize("L", [32, 4])
+def test_kevin_prepends(L):
+    # the reference's "kevin" benchmark shape (benches/yjs.rs:51-62): single-char prepends at
+    # position 0, one unmergeable entry each.  200k prepends at leaf 4 = 50,000 leaves, past the
+    # round-1 directory limit (8,160 leaves); tests/test_gpu_parity.py runs 1M on the GPU.
+    n = 200_000
+    c = np.ones(n, np.uint32)
+    p = np.zeros((n, 3), np.uint32)
+    p[:, 2] = 1
+    o = OracleDoc(L, 16 if L == 32 else 8)
+    assert o.apply_trace(o.agent("seph"), c, p) == 0
+    e = EmuDoc(L)
+    assert e.run_local(e.agent("seph"), c, p, 48 if L == 32 else 4) == 0
+    assert e.check() == ""
+    assert diff_states(o.export(), e.export()) == []
+
+
+@pytest.mark.parametrize("L", [32, 4])
+def test_config5_full_size(L):
+    # BASELINE config 5 at its stated size: a 1M-char base, 16 agents x 64 rounds x 64 txns
+    # (65,536 remote txns); the frontier grows past its first capacity (16 heads), the debug
+    # layout needs ~23k leaves.
+    from fuzz_gen import config5_wire
+    w = config5_wire(7, base_len=1 << 20, n_agents=16, rounds=64, ops=64)
+    o = OracleDoc(L, 16 if L == 32 else 8)
+    assert o.apply_remote_wire(w) == 0
+    e = EmuDoc(L)
+    assert e.run_wire(w, 48) == 0
+    assert e.check() == ""
+    assert diff_states(o.export(), e.export()) == []
+    assert e.sizes()["frontier"] == 16 and e.sizes()["grow_mask"] & 128

@@ -47,6 +47,24 @@ def check_queries(e, doc, o):
         assert np.array_equal(gp[od != 2], op[od != 2])
 
 
+def check_queries_sampled(e, doc, o, n=1 << 18, seed=5):
+    """check_queries for large documents: n random positions (plus both ends) and n random
+    (agent, seq) pairs over every agent's seq range, against the oracle."""
+    rng = np.random.default_rng(seed)
+    ln = len(o)
+    pos = np.concatenate([rng.integers(0, ln + 2, n), [0, max(ln - 1, 0), ln, ln + 1]]).astype(np.uint32)
+    ga, gs = e.pos_to_loc(np.full(pos.shape, doc, np.uint32), pos)
+    oa, os_ = o.pos_to_loc(pos)
+    assert np.array_equal(ga, oa) and np.array_equal(gs, os_)
+    s = o.sizes()
+    ag = rng.integers(0, s["agents"], n).astype(np.uint16)
+    seq = rng.integers(0, s["next_order"] + 1, n).astype(np.uint32)
+    gp, gd = e.loc_to_pos(np.full(seq.shape, doc, np.uint32), ag, seq)
+    op, od = o.loc_to_pos(ag, seq)
+    assert np.array_equal(gd, od)
+    assert np.array_equal(gp[od != 2], op[od != 2])
+
+
 @pytest.mark.parametrize("name", ["sveltecomponent", "rustcode", "automerge-paper"])
 def test_trace_local_exact(name):
     t = load_trace(name)
@@ -76,8 +94,9 @@ def test_trace_remote_exact(name):
     check_queries(e, 1, o)
 
 
-@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode"])
+@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode", "automerge-paper"])
 def test_trace_debug_layout(name):
+    # automerge-paper at leaf 4 needs ~25,900 leaves: past round 1's 8,160-leaf directory
     t = load_trace(name)
     e = crdt_amd.Engine(1, 4)
     a = e.agent_intern([0], ["jeremy"])
@@ -228,3 +247,52 @@ def test_mixed_corpus_config3():
     dg = e.digests()
     for d in range(n):
         assert int(dg[d]) == int(gold[f"{names[which[d]]}/L32"]["digest"], 16), d
+
+
+def test_kevin_prepends():
+    # the reference's "kevin" benchmark shape (benches/yjs.rs:51-62), 1M single-char prepends at
+    # position 0: 31,250 leaves at the release layout, 250,000 at the debug layout (an LDS root
+    # class of its own, one wave per workgroup).  A small document in the same engine takes the
+    # default root class: two replay launches from one run, with document lists.
+    n = 1_000_000
+    c = np.ones(n, np.uint32)
+    p = np.zeros((n, 3), np.uint32)
+    p[:, 2] = 1
+    sv = load_trace("sveltecomponent")
+    for L in (32, 4):
+        e = crdt_amd.Engine(2, L)
+        ag = e.agent_intern([0, 1], ["seph", "jeremy"])
+        tx = np.concatenate([np.stack([np.full(n, ag[0]), c], 1),
+                             np.stack([np.full(len(sv.counts), ag[1]), sv.counts], 1)]).astype(np.uint32)
+        st = e.apply_local_arrays([0, 1], [0, n, n + len(sv.counts)], tx, np.concatenate([p, sv.patches]))
+        assert (st == 0).all(), st
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        assert o.apply_trace(o.agent("seph"), c, p) == 0
+        assert_same(e.export(0), o.export())
+        assert int(e.digests()[0]) == o.digest()
+        o2 = OracleDoc(L, 16 if L == 32 else 8)
+        assert o2.apply_trace(o2.agent("jeremy"), sv.counts, sv.patches) == 0
+        assert int(e.digests()[1]) == o2.digest()
+        check_queries_sampled(e, 0, o)
+
+
+def test_config5_full_size():
+    # BASELINE config 5 at its stated size: per document a 1M-char base by agent
+    # "base", then 16 agents x 64 rounds x 64 concurrent txns = 65,536 remote txns (60 % deletes
+    # of 1..64 base items -> double deletes, 40 % inserts at 32 shared hotspots -> integrate ties),
+    # seeded delivery order.  Bit-exact against the oracle, at both layouts.
+    from fuzz_gen import config5_wire
+    wires = [config5_wire(900 + s, base_len=1 << 20, n_agents=16, rounds=64, ops=64) for s in range(4)]
+    for L in (32, 4):
+        e = crdt_amd.Engine(len(wires), L)
+        st = e.apply_remote_wire(list(range(len(wires))), wires)
+        assert (st == 0).all(), st
+        dg = e.digests()
+        for i, w in enumerate(wires):
+            o = OracleDoc(L, 16 if L == 32 else 8)
+            assert o.apply_remote_wire(w) == 0
+            assert int(dg[i]) == o.digest(), (L, i)
+            if i < 2:
+                assert_same(e.export(i), o.export())
+            if i == 0:
+                check_queries_sampled(e, 0, o)

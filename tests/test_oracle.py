@@ -265,3 +265,32 @@ def test_text_matches_end_content(name, leaf, node):
     b = utf32_to_str(txt).encode()
     assert len(txt) == t.end_len and len(b) == t.end_bytes
     assert fnv1a64(b) == t.end_fnv
+
+
+@pytest.mark.parametrize("name", ["sveltecomponent", "rustcode", "automerge-paper"])
+def test_splitlist_index_same_state(name):
+    # the CPU baseline's order index is the reference's SplitList (split_list/mod.rs, bucket 100,
+    # delete orders padded with the last marker, doc.rs:337-339 / 402-404); it must give the same
+    # document as the dense table, on the local and the remote (index-reading) path
+    from crdt_amd.traces import load_remote_wire
+    t = load_trace(name)
+    a = OracleDoc(32, 16)
+    b = OracleDoc(32, 16, split_index=True)
+    assert a.apply_trace(a.agent("jeremy"), t.counts, t.patches) == 0
+    assert b.apply_trace(b.agent("jeremy"), t.counts, t.patches) == 0
+    assert a.digest() == b.digest()
+    w = load_remote_wire(name)
+    a, b = OracleDoc(32, 16), OracleDoc(32, 16, split_index=True)
+    assert a.apply_remote_wire(w) == 0 and b.apply_remote_wire(w) == 0
+    assert a.digest() == b.digest()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_splitlist_index_concurrent(seed):
+    from fuzz_gen import concurrent_wire, config5_wire
+    for w in (concurrent_wire(seed, n_agents=3, rounds=5)[0], config5_wire(seed, base_len=2000, rounds=4, ops=4)):
+        a, b = OracleDoc(4, 8), OracleDoc(4, 8, split_index=True)
+        sa, sb = a.apply_remote_wire(w), b.apply_remote_wire(w)
+        assert sa == sb
+        if sa == 0:
+            assert a.digest() == b.digest()

@@ -103,6 +103,7 @@ def lib():
     L.crdt_stream.restype = vp
     L.crdt_set_content.argtypes = [vp, u64, P(u32), P(u32), u32, P(u64), P(u32)]
     L.crdt_materialize_async.argtypes = [vp]
+    L.crdt_set_content_copies.argtypes = [vp, u64, P(u32), P(u32), u64]
     L.crdt_text.argtypes = [vp, u32, P(u32), u64, P(u64)]
     L.crdt_text_digest.argtypes = [vp, P(u64)]
     L.crdt_last_materialize_ms.argtypes = [vp, P(C.c_double)]
@@ -125,7 +126,7 @@ EXPORTED_SYMBOLS = [
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
-    "crdt_last_materialize_ms",
+    "crdt_last_materialize_ms", "crdt_set_content_copies",
     # include/crdt_trace.h (host-only trace ingestion)
     "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
@@ -189,7 +190,15 @@ class Engine:
                 np.concatenate(ops).astype(np.uint32) if ops else np.zeros((0, 3), np.uint32))
 
     def apply_local(self, per_doc) -> np.ndarray:
-        d, off, tx, ops = self._local_arrays(per_doc)
+        return self.apply_local_arrays(*self._local_arrays(per_doc))
+
+    def apply_local_arrays(self, d, off, tx, ops) -> np.ndarray:
+        """crdt_apply_local on CSR arrays: docs [n], txn_off [n+1] (u64), txns [T,2] (agent, n_ops),
+        ops [sum n_ops, 3] (pos, del, ins)."""
+        d = np.ascontiguousarray(d, dtype=np.uint32)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        tx = np.ascontiguousarray(tx, dtype=np.uint32).reshape(-1, 2)
+        ops = np.ascontiguousarray(ops, dtype=np.uint32).reshape(-1, 3)
         st = np.zeros(d.shape[0], np.int32)
         _check(self.L.crdt_apply_local(self.h, d.shape[0], _p(d), _p(off, C.c_uint64), tx.ctypes.data,
                                        ops.ctypes.data, _p(st, C.c_int32)), "apply_local")
@@ -256,7 +265,7 @@ class Engine:
         return st[np.asarray(docs, dtype=np.int64)]
 
     def debug_state(self, doc: int) -> np.ndarray:
-        out = np.zeros(22, np.uint32)
+        out = np.zeros(23, np.uint32)
         _check(self.L.crdt_debug_state(self.h, doc, _p(out)), "debug_state")
         return out
 
@@ -311,6 +320,13 @@ class Engine:
                "loc_to_pos")
         return p, dl
 
+    def export_sizes(self, doc: int) -> dict:
+        s = np.zeros(12, np.uint64)
+        _check(self.L.crdt_export_sizes(self.h, doc, _p(s, C.c_uint64)), "export_sizes")
+        keys = ["raw", "leaves", "canon", "cwo", "deletes", "dd", "txns", "parents", "frontier", "agents",
+                "next_order", "len"]
+        return {k: int(v) for k, v in zip(keys, s)}
+
     def export(self, doc: int) -> dict:
         s = np.zeros(12, np.uint64)
         _check(self.L.crdt_export_sizes(self.h, doc, _p(s, C.c_uint64)), "export_sizes")
@@ -339,6 +355,12 @@ class Engine:
                                     if streams else np.zeros(0, np.uint32))
         _check(self.L.crdt_set_content(self.h, d.shape[0], _p(d), _p(so), len(streams), _p(off, C.c_uint64),
                                        _p(data)), "set_content")
+
+    def set_content_copies(self, docs: Sequence[int], content: np.ndarray):
+        """every docs[i] gets its own device copy of one order-indexed UTF-32 table"""
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        c = np.ascontiguousarray(content, dtype=np.uint32)
+        _check(self.L.crdt_set_content_copies(self.h, d.shape[0], _p(d), _p(c), c.shape[0]), "set_content_copies")
 
     def materialize_async(self):
         _check(self.L.crdt_materialize_async(self.h), "materialize")

@@ -29,9 +29,14 @@ constexpr u32 UNKNOWN_AGENT = 0xFFFEu;    // a name that is not (yet) interned f
 constexpr u32 INVALID = 0xFFFFFFFFu;
 
 constexpr u32 GROUP = 64;                 // directory slots per block (one wavefront)
-constexpr u32 MAX_GROUP_REGS = 4;         // root level: up to 4 x 64 groups in VGPRs
-constexpr u32 MAX_GROUPS = GROUP * MAX_GROUP_REGS;
-constexpr u32 FRONTIER_CAP = 64;
+// Root level of the directory: one group (block id, slot count, visible count) per directory
+// block, held in LDS while a wave replays its document.  Its size per wave is chosen per launch
+// (a multiple of 64 groups, 12 B each): a single one-wave workgroup may declare all 160 KiB of a
+// CU's LDS, so a document can have up to ROOT_CAP_MAX blocks = at least 32*(ROOT_CAP_MAX-1)
+// leaves (every block but the first holds >= 32 slots) = 13.9M entries at the release layout.
+constexpr u32 ROOT_CAP_MIN = 256;
+constexpr u32 ROOT_CAP_MAX = 13632;       // floor(163840 / 12 / 64) * 64
+constexpr u32 FRONTIER_CAP0 = 4;          // initial frontier capacity (grows on demand)
 
 // Status codes (identical to include/crdt_gpu.h and the oracle)
 enum : i32 {
@@ -80,6 +85,10 @@ struct CwoRun { u32 key, agent, seq, len; };   // client_with_order
 struct ARun { u32 key, order, len, pad; };     // item_orders of one agent (seq -> order)
 struct DelRun { u32 key, order, len; };        // deletes
 struct DDRun { u32 key, len, excess; };        // double_deletes
+// The double-delete RLE is kept in 64-entry blocks (physical block p = entries [64p, 64p+64))
+// ordered by a block directory, so an insertion shifts one block, not the table's tail.
+constexpr u32 DD_BLK = 64;
+struct DDBlk { u32 phys, first, cnt, pad; };   // physical block, first key, entries
 struct TxnRec { u32 order, len, shadow, poff, pn, pad[3]; };  // txns (32 B)
 struct AgentRec { u32 run_base, run_cnt, run_cap, rank; };   // per-document agent table
 struct GroupRec { u32 blk, cnt, vis, pad; };   // persisted root level of the directory
@@ -134,10 +143,12 @@ struct DocSeg {
   u64 blk_base;    // first directory block; slots at blk_base*64
   u64 map_base;    // order -> leaf table (u32 per order)
   u64 cwo_base, arun_base, del_base, dd_base, txn_base, par_base, fr_base, agent_base, grp_base;
+  // dd_base / dd_cap count double-delete BLOCKS: directory at ddb[dd_base], entries at dd[dd_base*64]
   u64 rec_base;    // first record of this call's stream
   u32 leaf_cap, blk_cap, map_cap, cwo_cap;
   u32 arun_cap, del_cap, dd_cap, txn_cap;
   u32 par_cap, agent_cap, rec_n, flags;
+  u32 fr_cap, grp_cap;  // frontier heads; root groups (= blk_cap)
 };
 
 struct DocState {
@@ -148,6 +159,7 @@ struct DocState {
   u32 n_del, n_dd, n_txn, n_par;
   u32 n_fr, n_agents, n_items, cap_need;
   u32 n_entries, gen_done;  // gen_done: ops of the current GEN record applied
+  u32 n_ddb;                // double-delete blocks in use
   u32 prof0, prof1, prof2, prof3;  // diagnostic cycle counters (-DCRDT_PROF builds only)
 };
 
@@ -161,11 +173,12 @@ struct Pools {
   ARun* arun;
   DelRun* dels;
   DDRun* dd;
+  DDBlk* ddb;
   TxnRec* txns;
   u32* parents;
-  u32* frontier;       // [fr_base .. + FRONTIER_CAP]
+  u32* frontier;       // [fr_base .. + fr_cap]
   AgentRec* agents;
-  GroupRec* groups;    // [grp_base .. + MAX_GROUPS]
+  GroupRec* groups;    // [grp_base .. + grp_cap]
   const Rec* recs;
   const DocSeg* seg;
   DocState* st;

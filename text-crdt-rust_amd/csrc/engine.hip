@@ -53,8 +53,11 @@ struct PoolSet {
   ARun* arun = nullptr;
   DelRun* dels = nullptr;
   DDRun* dd = nullptr;
+  DDBlk* ddb = nullptr;
   TxnRec* txns = nullptr;
   u32* parents = nullptr;
+  u32* frontier = nullptr;
+  GroupRec* groups = nullptr;
   AgentRec* agents = nullptr;
   Span* canon = nullptr;
   u32* vpos = nullptr;
@@ -62,18 +65,41 @@ struct PoolSet {
   u64 bytes = 0;
   void free_all() {
     dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(cwo); dfree(arun);
-    dfree(dels); dfree(dd); dfree(txns); dfree(parents); dfree(agents); dfree(canon); dfree(vpos); dfree(span_of);
+    dfree(dels); dfree(dd); dfree(ddb); dfree(txns); dfree(parents); dfree(frontier); dfree(groups); dfree(agents); dfree(canon);
+    dfree(vpos); dfree(span_of);
     bytes = 0;
   }
 };
 
 struct DocHost {
   AgentTable agents;
-  StreamNeeds cum;          // cumulative needs of everything applied since the last reset
-  Caps caps{};              // current capacities
+  StreamNeeds cum;          // needs of every stream applied since the last reset (capacity plan)
+  StreamNeeds staged;       // needs of the stream staged now (a reset replays it: cum = staged)
+  Caps caps{};              // current capacities (never shrink)
   std::vector<u32> agent_cap;
-  bool sized = false;
 };
+
+inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
+  c.n_txn += n.n_txn; c.n_ltxn += n.n_ltxn; c.n_rtxn += n.n_rtxn; c.n_ops += n.n_ops; c.orders += n.orders;
+  c.local_del += n.local_del; c.remote_del_ops += n.remote_del_ops; c.remote_parents += n.remote_parents;
+  if (c.txns_per_agent.size() < n.txns_per_agent.size()) c.txns_per_agent.resize(n.txns_per_agent.size(), 0);
+  for (size_t a = 0; a < n.txns_per_agent.size(); a++) c.txns_per_agent[a] += n.txns_per_agent[a];
+}
+
+// Launch shape of a wave-per-document kernel whose waves hold an LDS root of `rcap` groups:
+// up to 4 waves per workgroup within the 160 KiB a workgroup may declare.
+struct LaunchShape { u32 wpb, rcap; size_t lds; };
+inline LaunchShape launch_shape(u32 rcap) {
+  u32 per_wave = 12u * rcap;
+  u32 wpb = std::max<u32>(1u, std::min<u32>(WAVES_PER_BLOCK, 163840u / per_wave));
+  return LaunchShape{wpb, rcap, (size_t)wpb * per_wave};
+}
+// LDS root classes: a launch serves documents whose root fits its class.
+constexpr u32 ROOT_CLASSES[4] = {ROOT_CAP_MIN, 1024, 4096, ROOT_CAP_MAX};
+inline u32 root_class(u32 grp_cap) {
+  for (u32 c : ROOT_CLASSES) if (grp_cap <= c) return c;
+  return 0;  // cannot be held (the host never plans this)
+}
 
 }  // namespace
 
@@ -89,12 +115,15 @@ struct crdt_engine {
   // fixed per-document buffers
   DocState* st = nullptr;
   DocSeg* segs = nullptr;
-  u32* frontier = nullptr;
-  GroupRec* groups = nullptr;
   u32* canon_n = nullptr;
   u32* len = nullptr;
   u64* digest = nullptr;
   u32* n_agents_d = nullptr;
+  std::vector<u32> n_agents_pushed;  // host copy of what n_agents_d holds
+  // replay launches: one per LDS root class present; `doc_list` holds the classes' documents
+  struct RootClass { u32 rcap; u64 off, n; };
+  std::vector<RootClass> classes;
+  u32* doc_list = nullptr;
   PoolSet pools;
   Rec* recs = nullptr;
   u64 rec_cap = 0;
@@ -127,11 +156,12 @@ struct crdt_engine {
     p.arun = ps.arun;
     p.dels = ps.dels;
     p.dd = ps.dd;
+    p.ddb = ps.ddb;
     p.txns = ps.txns;
     p.parents = ps.parents;
-    p.frontier = frontier;
+    p.frontier = ps.frontier;
     p.agents = ps.agents;
-    p.groups = groups;
+    p.groups = ps.groups;
     p.recs = recs;
     p.seg = segs;
     p.st = st;
@@ -150,7 +180,9 @@ struct crdt_engine {
 
   void release() {
     pools.free_all();
-    dfree(st); dfree(segs); dfree(frontier); dfree(groups); dfree(canon_n); dfree(len); dfree(digest); dfree(n_agents_d);
+    dfree(st); dfree(segs); dfree(canon_n); dfree(len); dfree(digest); dfree(n_agents_d); dfree(doc_list);
+    n_agents_pushed.clear();
+    classes.clear();
     dfree(recs);
     rec_cap = 0;
     dfree(content); dfree(cbase); dfree(clen); dfree(text); dfree(tlen); dfree(tdigest);
@@ -178,8 +210,6 @@ struct crdt_engine {
     st_h.assign(n, DocState{});
     HIPCHK(dalloc(st, n));
     HIPCHK(dalloc(segs, n));
-    HIPCHK(dalloc(frontier, n * FRONTIER_CAP));
-    HIPCHK(dalloc(groups, n * MAX_GROUPS));
     HIPCHK(dalloc(canon_n, n));
     HIPCHK(dalloc(len, n));
     HIPCHK(dalloc(digest, n));
@@ -203,8 +233,9 @@ struct crdt_engine {
   // Assign per-document bases from docs[].caps into a fresh PoolSet; if `move`, relocate the
   // existing state into it (k_relayout), else just install it.
   int layout(bool move) {
+    int r = 0;
     PoolSet np;
-    u64 nl = 0, nb = 0, nm = 0, nc = 0, na = 0, ndl = 0, ndd = 0, nt = 0, npar = 0, nag = 0;
+    u64 nl = 0, nb = 0, nm = 0, nc = 0, na = 0, ndl = 0, ndd = 0, nt = 0, npar = 0, nag = 0, nfr = 0;
     std::vector<DocSeg> nseg(n_docs);
     std::vector<AgentRec> agent_tab;
     std::vector<u32> n_agents(n_docs);
@@ -220,8 +251,8 @@ struct crdt_engine {
       s.dd_base = ndd; s.dd_cap = c.dd; ndd += c.dd;
       s.txn_base = nt; s.txn_cap = c.txn; nt += c.txn;
       s.par_base = npar; s.par_cap = c.par; npar += c.par;
-      s.fr_base = d * FRONTIER_CAP;
-      s.grp_base = d * MAX_GROUPS;
+      s.fr_base = nfr; s.fr_cap = c.fr; nfr += c.fr;
+      s.grp_base = s.blk_base; s.grp_cap = c.blk;  // one root group per directory block
       s.agent_base = nag;
       u32 ag = (u32)h.agents.names.size();
       s.agent_cap = ag;
@@ -254,14 +285,17 @@ struct crdt_engine {
     HIPCHK(dalloc(np.cwo, nc));
     HIPCHK(dalloc(np.arun, na));
     HIPCHK(dalloc(np.dels, ndl));
-    HIPCHK(dalloc(np.dd, ndd));
+    HIPCHK(dalloc(np.dd, ndd * DD_BLK));
+    HIPCHK(dalloc(np.ddb, ndd));
     HIPCHK(dalloc(np.txns, nt));
     HIPCHK(dalloc(np.parents, npar));
+    HIPCHK(dalloc(np.frontier, nfr));
+    HIPCHK(dalloc(np.groups, nb));
     HIPCHK(dalloc(np.agents, nag));
     HIPCHK(dalloc(np.canon, nl * L));
     HIPCHK(dalloc(np.vpos, nl * L));
-    np.bytes = nl * L * (16 + 16 + 4) + nl * 4 + nb * GROUP * 8 + nm * 8 + nc * 16 + na * 16 + ndl * 12 + ndd * 12 +
-               nt * 32 + npar * 4 + nag * 16;
+    np.bytes = nl * L * (16 + 16 + 4) + nl * 4 + nb * GROUP * 8 + nm * 8 + nc * 16 + na * 16 + ndl * 12 + ndd * (DD_BLK * 12 + 16) +
+               nt * 32 + npar * 4 + nag * 16 + nfr * 4 + nb * 16;
     if (!agent_tab.empty())
       HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(n_agents_d, n_agents.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
@@ -284,20 +318,63 @@ struct crdt_engine {
     pools.free_all();
     pools = np;
     seg_h = nseg;
+    r = plan_classes();
+    if (r) return r;
     map_total = nm;
     published = false;
     materialized = false;
     return 0;
   }
 
+  // Replay launch classes (LDS root sizes) from the documents' root capacities; the documents
+  // of every class go to the device list when more than one class is present.
+  int plan_classes() {
+    std::vector<std::vector<u32>> by(4);
+    for (u64 d = 0; d < n_docs; d++) {
+      u32 c = root_class(seg_h[d].grp_cap);
+      u32 k = 0;
+      while (ROOT_CLASSES[k] != c) k++;
+      by[k].push_back((u32)d);
+    }
+    classes.clear();
+    dfree(doc_list);
+    u32 present = 0;
+    for (auto& v : by) present += !v.empty();
+    if (present <= 1) {
+      for (u32 k = 0; k < 4; k++)
+        if (!by[k].empty()) classes.push_back(RootClass{ROOT_CLASSES[k], INVALID, by[k].size()});
+      return 0;
+    }
+    std::vector<u32> all;
+    for (u32 k = 0; k < 4; k++) {
+      if (by[k].empty()) continue;
+      classes.push_back(RootClass{ROOT_CLASSES[k], all.size(), by[k].size()});
+      all.insert(all.end(), by[k].begin(), by[k].end());
+    }
+    HIPCHK(dalloc(doc_list, all.size()));
+    HIPCHK(hipMemcpyAsync(doc_list, all.data(), all.size() * 4, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    return 0;
+  }
+
+  // Every document to ListCRDT::new().  Agents interned since the last layout get their table
+  // slots first (a relayout; the old state is discarded anyway).
   int init_all() {
+    bool relayout = false;
+    for (u64 d = 0; d < n_docs; d++)
+      if (docs[d].agents.names.size() != seg_h[d].agent_cap) relayout = true;
+    if (relayout) {
+      int r = layout(false);
+      if (r) return r;
+    }
     // host-side agent counts into the state before k_init (k_init keeps n_agents)
     int r = push_agent_counts();
     if (r) return r;
-    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    LaunchShape sh = launch_shape(64);
+    u32 blocks = (u32)((n_docs + sh.wpb - 1) / sh.wpb);
     if (n_docs) {
-      if (L == 32) hipLaunchKernelGGL(k_init<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
-      else hipLaunchKernelGGL(k_init<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
+      if (L == 32) hipLaunchKernelGGL(k_init<32>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pools_view(pools), (u32)n_docs, sh.wpb, sh.rcap);
+      else hipLaunchKernelGGL(k_init<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pools_view(pools), (u32)n_docs, sh.wpb, sh.rcap);
       HIPCHK(hipGetLastError());
     }
     published = false;
@@ -305,11 +382,17 @@ struct crdt_engine {
     return 0;
   }
 
+  // st[d].n_agents := the host's interned count for every document (clamped to the document's
+  // agent table, which layout() sized).  Uploaded only when it changed; the host copy outlives
+  // the asynchronous copy (the stream is synchronised right after it).
   int push_agent_counts() {
-    // write st[d].n_agents (field offset) for every document
     std::vector<u32> na(n_docs);
-    for (u64 d = 0; d < n_docs; d++) na[d] = (u32)docs[d].agents.names.size();
-    HIPCHK(hipMemcpyAsync(n_agents_d, na.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
+    for (u64 d = 0; d < n_docs; d++) na[d] = std::min<u32>((u32)docs[d].agents.names.size(), seg_h[d].agent_cap);
+    if (na != n_agents_pushed) {
+      n_agents_pushed = na;
+      HIPCHK(hipMemcpyAsync(n_agents_d, n_agents_pushed.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
     if (n_docs) {  // one launch for every document (not one 4-byte copy per document)
       hipLaunchKernelGGL(k_set_n_agents, dim3((u32)((n_docs + 255) / 256)), dim3(256), 0, stream, st, (const u32*)n_agents_d, (u32)n_docs);
       HIPCHK(hipGetLastError());
@@ -322,21 +405,29 @@ struct crdt_engine {
     int r = set_device();
     if (r) return r;
     HIPCHK(hipStreamSynchronize(stream));
+    // a stage replaces every document's staged stream (documents not named get none)
+    {
+      std::vector<char> seen(n_docs, 0);
+      for (u64 d : doc_ids) {
+        if (seen[d]) return CRDT_E_ARG;  // a document named twice in one call
+        seen[d] = 1;
+      }
+      for (u64 d = 0; d < n_docs; d++)
+        if (!seen[d]) docs[d].staged = StreamNeeds{};
+    }
     // cumulative needs -> capacities
     bool grow = false;
     for (size_t i = 0; i < doc_ids.size(); i++) {
       DocHost& h = docs[doc_ids[i]];
       StreamNeeds& c = h.cum;
-      const StreamNeeds& n = needs[i];
-      c.n_txn += n.n_txn; c.n_ltxn += n.n_ltxn; c.n_rtxn += n.n_rtxn; c.n_ops += n.n_ops; c.orders += n.orders;
-      c.local_del += n.local_del; c.remote_del_ops += n.remote_del_ops; c.remote_parents += n.remote_parents;
-      if (c.txns_per_agent.size() < n.txns_per_agent.size()) c.txns_per_agent.resize(n.txns_per_agent.size(), 0);
-      for (size_t a = 0; a < n.txns_per_agent.size(); a++) c.txns_per_agent[a] += n.txns_per_agent[a];
+      add_needs(c, needs[i]);
+      h.staged = needs[i];
       Caps nc = plan_caps(c, (u32)h.agents.names.size(), true, 48);
       Caps& oc = h.caps;
       auto up = [&](u32& o, u32 v) { if (v > o) { o = v; grow = true; } };
       up(oc.leaf, nc.leaf); up(oc.blk, nc.blk); up(oc.map, nc.map); up(oc.cwo, nc.cwo); up(oc.arun, nc.arun);
       up(oc.del, nc.del); up(oc.dd, nc.dd); up(oc.txn, nc.txn); up(oc.par, nc.par); up(oc.agent, nc.agent);
+      up(oc.fr, nc.fr);
       for (size_t a = 0; a < h.agents.names.size(); a++) {
         u32 t = a < c.txns_per_agent.size() ? c.txns_per_agent[a] : 0;
         u32 need = std::min<u32>(t + 1, 64 + t / 64);
@@ -417,11 +508,16 @@ struct crdt_engine {
   }
 
   int launch_replay() {
-    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     if (!n_docs) return 0;
-    if (L == 32) hipLaunchKernelGGL(k_replay<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
-    else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), (u32)n_docs);
-    HIPCHK(hipGetLastError());
+    Pools pv = pools_view(pools);
+    for (const RootClass& c : classes) {  // one launch per LDS root class (usually one)
+      LaunchShape sh = launch_shape(c.rcap);
+      u32 blocks = (u32)((c.n + sh.wpb - 1) / sh.wpb);
+      const u32* list = c.off == INVALID ? nullptr : doc_list + c.off;
+      if (L == 32) hipLaunchKernelGGL(k_replay<32>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+      else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+      HIPCHK(hipGetLastError());
+    }
     published = false;
     materialized = false;
     return 0;
@@ -456,20 +552,21 @@ struct crdt_engine {
         if (need & 1u) {
           if (c.leaf >= MAX_LEAVES) { need &= ~1u; }
           c.leaf = std::min<u32>(c.leaf * 2, MAX_LEAVES);
-          c.blk = c.leaf / 32 + 2;
+          c.blk = blk_cap_for(c.leaf);
         }
+        if (need & 128u) c.fr = c.fr * 2;
         if (need & 2u) { c.cwo = c.cwo * 2 + 1; c.txn = c.txn * 2 + 1; }
         if (need & 4u) c.del = c.del * 2 + 16;
         if (need & 8u) c.par = c.par * 2 + 16;
         if (need & 16u) c.map = c.map * 2 + 16;
-        if (need & 64u) c.dd = c.dd * 2 + 64;
+        if (need & 64u) c.dd = c.dd * 2 + 2;
         if (need & 32u) for (auto& x : docs[d].agent_cap) x = x * 2 + 1;
         if (need == 0) {  // cannot grow: make it a hard capacity error
-          DocState s = st_h[d];
-          s.status = ST_CAPACITY;
-          HIPCHK(hipMemcpyAsync(&st[d].status, &s.status, 4, hipMemcpyHostToDevice, stream));
+          st_h[d].status = ST_CAPACITY;
+          HIPCHK(hipMemcpyAsync(&st[d].status, &st_h[d].status, 4, hipMemcpyHostToDevice, stream));
         }
       }
+      HIPCHK(hipStreamSynchronize(stream));
       if (!any) break;
       r = layout(true);
       if (r) return r;
@@ -525,6 +622,10 @@ struct crdt_engine {
       if (docs[i] >= n_docs || stream_of_doc[i] >= n_streams) return CRDT_E_ARG;
     u64 total = stream_off[n_streams];
     HIPCHK(hipStreamSynchronize(stream));
+    if (total == 0) {  // no content: release the table
+      dfree(content);
+      content_cap = 0;
+    }
     if (total > content_cap) {
       dfree(content);
       HIPCHK(dalloc(content, total));
@@ -537,6 +638,40 @@ struct crdt_engine {
       u32 k = stream_of_doc[i];
       cbase_h[docs[i]] = stream_off[k];
       clen_h[docs[i]] = stream_off[k + 1] - stream_off[k];
+    }
+    HIPCHK(hipMemcpyAsync(cbase, cbase_h.data(), n_docs * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemcpyAsync(clen, clen_h.data(), n_docs * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    materialized = false;
+    return 0;
+  }
+  // Every listed document gets its own device copy of one content stream (a corpus whose documents
+  // do not share a cache-resident table).
+  int set_content_copies(u64 n, const uint32_t* docs, const uint32_t* data, u64 len) {
+    int r = set_device();
+    if (r) return r;
+    for (u64 i = 0; i < n; i++)
+      if (docs[i] >= n_docs) return CRDT_E_ARG;
+    u64 total = n * len;
+    HIPCHK(hipStreamSynchronize(stream));
+    if (total > content_cap || total == 0) {
+      dfree(content);
+      content_cap = 0;
+      if (total) {
+        HIPCHK(dalloc(content, total));
+        content_cap = total;
+      }
+    }
+    if (total) {
+      HIPCHK(hipMemcpyAsync(content, data, len * 4, hipMemcpyHostToDevice, stream));
+      for (u64 i = 1; i < n; i++)
+        HIPCHK(hipMemcpyAsync(content + i * len, content, len * 4, hipMemcpyDeviceToDevice, stream));
+    }
+    std::fill(cbase_h.begin(), cbase_h.end(), NO_CONTENT);
+    std::fill(clen_h.begin(), clen_h.end(), 0);
+    for (u64 i = 0; i < n; i++) {
+      cbase_h[docs[i]] = i * len;
+      clen_h[docs[i]] = len;
     }
     HIPCHK(hipMemcpyAsync(cbase, cbase_h.data(), n_docs * 8, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(clen, clen_h.data(), n_docs * 8, hipMemcpyHostToDevice, stream));
@@ -604,6 +739,9 @@ int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
   e->device = cfg->device;
   if (hipSetDevice(e->device) != hipSuccess) return CRDT_E_DEVICE;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return CRDT_E_DEVICE;
+  // the replay's LDS root may take a workgroup's whole 160 KiB (one wave per workgroup)
+  (void)hipFuncSetAttribute((const void*)k_replay<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return CRDT_E_DEVICE;
   *out = e.release();
@@ -779,6 +917,8 @@ int crdt_reset_async(crdt_engine* e) {
   if (!valid(e)) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
+  // capacities planned from now on cover the histories since this reset: the staged streams
+  for (auto& h : e->docs) h.cum = h.staged;
   hipLaunchKernelGGL(k_reset_recpos, dim3((u32)((e->n_docs + 255) / 256)), dim3(256), 0, e->stream, e->st, (u32)e->n_docs, 0u);
   return e->init_all();
 }
@@ -959,7 +1099,7 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
   u32 L = e->L;
   if (raw4 || leaf_sizes) {
     std::vector<GroupRec> groups(st.ng);
-    HIPCHK(hipMemcpy(groups.data(), e->groups + sg.grp_base, st.ng * sizeof(GroupRec), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(groups.data(), e->pools.groups + sg.grp_base, st.ng * sizeof(GroupRec), hipMemcpyDeviceToHost));
     std::vector<u32> dl((size_t)st.n_blocks * GROUP);
     HIPCHK(hipMemcpy(dl.data(), e->pools.dir_leaf + sg.blk_base * GROUP, dl.size() * 4, hipMemcpyDeviceToHost));
     std::vector<Span> lv((size_t)st.n_leaves * L);
@@ -983,7 +1123,15 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
   if (canon4 && s[2]) HIPCHK(hipMemcpy(canon4, e->pools.canon + sg.leaf_base * L, s[2] * 16, hipMemcpyDeviceToHost));
   if (cwo4 && st.n_cwo) HIPCHK(hipMemcpy(cwo4, e->pools.cwo + sg.cwo_base, st.n_cwo * 16, hipMemcpyDeviceToHost));
   if (del3 && st.n_del) HIPCHK(hipMemcpy(del3, e->pools.dels + sg.del_base, st.n_del * 12, hipMemcpyDeviceToHost));
-  if (dd3 && st.n_dd) HIPCHK(hipMemcpy(dd3, e->pools.dd + sg.dd_base, st.n_dd * 12, hipMemcpyDeviceToHost));
+  if (dd3 && st.n_dd) {  // flatten the blocks in directory order
+    std::vector<DDBlk> dir(st.n_ddb);
+    std::vector<DDRun> ent((size_t)st.n_ddb * DD_BLK);
+    HIPCHK(hipMemcpy(dir.data(), e->pools.ddb + sg.dd_base, dir.size() * sizeof(DDBlk), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ent.data(), e->pools.dd + sg.dd_base * DD_BLK, ent.size() * sizeof(DDRun), hipMemcpyDeviceToHost));
+    u64 k = 0;
+    for (const DDBlk& B : dir)
+      for (u32 i = 0; i < B.cnt && k < st.n_dd; i++, k++) std::memcpy(dd3 + 3 * k, &ent[(size_t)B.phys * DD_BLK + i], 12);
+  }
   if (txn5 && st.n_txn) {
     std::vector<TxnRec> t(st.n_txn);
     HIPCHK(hipMemcpy(t.data(), e->pools.txns + sg.txn_base, st.n_txn * sizeof(TxnRec), hipMemcpyDeviceToHost));
@@ -993,15 +1141,15 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
     }
   }
   if (parents && st.n_par) HIPCHK(hipMemcpy(parents, e->pools.parents + sg.par_base, st.n_par * 4, hipMemcpyDeviceToHost));
-  if (frontier && st.n_fr) HIPCHK(hipMemcpy(frontier, e->frontier + sg.fr_base, st.n_fr * 4, hipMemcpyDeviceToHost));
+  if (frontier && st.n_fr) HIPCHK(hipMemcpy(frontier, e->pools.frontier + sg.fr_base, st.n_fr * 4, hipMemcpyDeviceToHost));
   return 0;
 }
 
-int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out22) {
-  if (!valid(e) || doc >= e->n_docs || !out22) return CRDT_E_ARG;
+int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23) {
+  if (!valid(e) || doc >= e->n_docs || !out23) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
-  HIPCHK(hipMemcpyAsync(out22, e->st + doc, sizeof(DocState), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(out23, e->st + doc, sizeof(DocState), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return 0;
 }
@@ -1020,6 +1168,12 @@ int crdt_set_content(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, cons
   if (!valid(e) || (n_docs && (!docs || !stream_of_doc)) || !stream_off || (stream_off[n_streams] && !content))
     return CRDT_E_ARG;
   return e->set_content(n_docs, docs, stream_of_doc, n_streams, stream_off, content);
+}
+
+int crdt_set_content_copies(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* content,
+                            uint64_t len) {
+  if (!valid(e) || (n_docs && !docs) || (len && !content)) return CRDT_E_ARG;
+  return e->set_content_copies(n_docs, docs, content, len);
 }
 
 int crdt_materialize_async(crdt_engine* e) {

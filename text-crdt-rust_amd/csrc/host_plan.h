@@ -184,18 +184,26 @@ inline void encode_gen(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, u32 n_
 
 // Capacities for a fresh document that will apply `nd` (heuristic leaf capacity; everything
 // else is an upper bound).  Growth for leaves/blocks is handled by the caller on ST_CAPACITY.
-constexpr u32 MAX_LEAVES = 32 * (MAX_GROUPS - 1);  // root level holds <= MAX_GROUPS blocks
+// Leaves are bounded only by the LDS root: blk_cap = leaf_cap/32 + 2 <= ROOT_CAP_MAX groups.
+constexpr u32 MAX_LEAVES = 32 * (ROOT_CAP_MAX - 2);
 
 struct Caps {
-  u32 leaf, blk, map, cwo, arun, del, dd, txn, par, agent;
+  u32 leaf, blk, map, cwo, arun, del, dd, txn, par, agent, fr;
 };
+inline u32 blk_cap_for(u32 leaf_cap) { return leaf_cap / 32 + 2; }
+// LDS root groups per wave for a document with `blk_cap` directory blocks (a multiple of 64)
+inline u32 root_cap_for(u32 blk_cap) {
+  u32 r = (blk_cap + 63u) & ~63u;
+  return r < ROOT_CAP_MIN ? ROOT_CAP_MIN : r;
+}
 inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_div = 48) {
   Caps c;
   u64 leaves = 64 + nd.n_ops / leaf_div;
   c.leaf = (u32)std::min<u64>(leaves, 1 + 2 * nd.n_ops + 1);
   if (c.leaf < 64) c.leaf = 64;
   if (c.leaf > MAX_LEAVES) c.leaf = MAX_LEAVES;
-  c.blk = c.leaf / 32 + 2;
+  c.blk = blk_cap_for(c.leaf);
+  c.fr = FRONTIER_CAP0;
   c.map = track ? (u32)std::min<u64>(nd.orders + 1, 0xFFFFFFFFull) : 0;
   // RLE tables usually coalesce far below one run per txn; start small and grow on demand
   // (ST_NEED_CAPACITY is resumable), exact bounds otherwise.
@@ -205,8 +213,8 @@ inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_
   for (u32 a = 0; a < n_agents; a++) arun += (a < nd.txns_per_agent.size() ? nd.txns_per_agent[a] : 0) + 1;
   c.arun = (u32)arun;
   c.del = (u32)std::min<u64>(nd.local_del + nd.remote_del_ops + 1, 0xFFFFFFFFull);
-  c.dd = (u32)std::min<u64>(4 * nd.remote_del_ops + 64, 1u << 24);
-  c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + FRONTIER_CAP + 1, 1024 + (nd.remote_parents + nd.n_txn) / 64);
+  c.dd = nd.remote_del_ops ? 4u : 0u;  // double-delete blocks: grown on demand (rare but for config 5)
+  c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + 64 + 1, 1024 + (nd.remote_parents + nd.n_txn) / 64);
   c.agent = n_agents;
   return c;
 }

@@ -23,35 +23,43 @@ struct PubOut {
 
 #define WAVES_PER_BLOCK 4
 
-// LDS slice (directory root level) of the calling wave: blk/cnt/vis x MAX_GROUPS u32
-#define ROOT_LDS __shared__ u32 s_root[WAVES_PER_BLOCK][3 * MAX_GROUPS]
+// Dynamic LDS of the wave-per-document kernels: each wave's directory root, 3 x rcap u32
+// (launch shape: engine.hip launch_shape).
+extern __shared__ u32 s_dyn[];
 template <int L>
-__device__ __forceinline__ WaveGPU<L> wave_with_root(u32 (*s_root)[3 * MAX_GROUPS]) {
+__device__ __forceinline__ WaveGPU<L> wave_with_root(u32 rcap) {
   WaveGPU<L> w;
   // the LDS address space survives into the member: root accesses are ds_* (lgkmcnt only);
   // a generic pointer would make them flat ops, whose waits also drain every pending store
-  w.rt = (typename WaveGPU<L>::lds_u32*)s_root[uni(threadIdx.x >> 6)];
+  w.rcap = rcap;
+  w.rt = (typename WaveGPU<L>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * 3u * rcap);
   return w;
+}
+// Document of the calling wave: wave k of the launch takes list[k] (or k without a list).
+__device__ __forceinline__ u32 wave_doc(u32 wpb, const u32* list, u32 n, u32& d) {
+  u32 k = uni(blockIdx.x * wpb + (threadIdx.x >> 6));
+  if (k >= n) return 0;
+  d = list ? uni(list[k]) : k;
+  return 1;
 }
 
 template <int L>
-__global__ __launch_bounds__(256) void k_init(Pools P, u32 n) {
-  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
-  if (d >= n) return;
-  ROOT_LDS;
-  Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(s_root));
+__global__ __launch_bounds__(256) void k_init(Pools P, u32 n, u32 wpb, u32 rcap) {
+  u32 d;
+  if (!wave_doc(wpb, nullptr, n, d)) return;
+  Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(rcap));
   r.init_empty();
   AgentRec* ag = r.agents();
   for (u32 a = lane_id(); a < r.g(S_N_AGENTS); a += 64) ag[a].run_cnt = 0;
   r.finish();
 }
 
+// n: waves of this launch (documents in `list`, or the first n documents)
 template <int L>
-__global__ __launch_bounds__(256) void k_replay(Pools P, u32 n) {
-  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
-  if (d >= n) return;
-  ROOT_LDS;
-  Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(s_root));
+__global__ __launch_bounds__(256) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
+  u32 d;
+  if (!wave_doc(wpb, list, n, d)) return;
+  Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(rcap));
   WaveGPU<L>& w = r.w;
   if (r.status() == ST_NEED_CAPACITY) r.p(S_STATUS, (u32)ST_OK);  // resume after growth
   if (r.status() != ST_OK || r.g(S_REC_POS) >= r.rec_n()) {
@@ -95,9 +103,12 @@ __global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const Do
   if (w.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);
   bcopy(dst.cwo + w.cwo_base, src.cwo + o.cwo_base, s.n_cwo);
   bcopy(dst.dels + w.del_base, src.dels + o.del_base, s.n_del);
-  bcopy(dst.dd + w.dd_base, src.dd + o.dd_base, s.n_dd);
+  bcopy(dst.dd + w.dd_base * DD_BLK, src.dd + o.dd_base * DD_BLK, (u64)s.n_ddb * DD_BLK);
+  bcopy(dst.ddb + w.dd_base, src.ddb + o.dd_base, s.n_ddb);
   bcopy(dst.txns + w.txn_base, src.txns + o.txn_base, s.n_txn);
   bcopy(dst.parents + w.par_base, src.parents + o.par_base, s.n_par);
+  bcopy(dst.frontier + w.fr_base, src.frontier + o.fr_base, s.n_fr);
+  bcopy(dst.groups + w.grp_base, src.groups + o.grp_base, s.ng);
   for (u32 a = 0; a < s.n_agents; a++) {
     AgentRec ao = src.agents[o.agent_base + a];
     AgentRec an = dst.agents[w.agent_base + a];
@@ -130,9 +141,8 @@ template <int L>
 __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
   if (d >= n) return;
-  ROOT_LDS;
   __shared__ u32 s_flag[WAVES_PER_BLOCK][64];
-  WaveGPU<L> w = wave_with_root<L>(s_root);
+  WaveGPU<L> w;
   DocState s = w.ldT(P.st + d);
   DocSeg seg = w.ld_seg(P.seg + d);
   u32 l = lane_id();
@@ -143,7 +153,7 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   Span* canon = O.canon + seg.leaf_base * L;
   u32* vpos = O.vpos + seg.leaf_base * L;
   const Span* leaves = P.leaves + seg.leaf_base * L;
-  w.root_load(P.groups + seg.grp_base, s.ng);
+  const GroupRec* groups = P.groups + seg.grp_base;  // the root level, read in order from HBM
   // Canonical spans, one leaf per step, lane i = entry i: an entry starts a new span unless
   // YjsSpan::can_append(previous entry, entry) (span.rs:47-53; merging is transitive, so the
   // previous raw entry stands for the open span); span lengths are segmented sums of a prefix
@@ -152,7 +162,7 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   Span open{0, 0, 0, 0};
   u32 open_vpos = 0;
   for (u32 g = 0; g < s.ng; g++) {
-    u32 blk = w.root_blk(g), cnt = w.root_cnt(g);
+    u32 blk = uni(groups[g].blk), cnt = uni(groups[g].cnt);
     u32 mydl = P.dir_leaf[(seg.blk_base + blk) * GROUP + l];  // 64-slot row: always in bounds
     // 64/L leaves per step: lane l holds entry l%L of leaf i + l/L; the valid entries (packed at
     // the front of each leaf) are then compacted to lanes [0, nn) with one ds_permute, so the
@@ -269,10 +279,15 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
     DelRun r = dels[k];
     h += elem_hash(3, k, ((u64)r.key << 32) | r.order, r.len);
   }
-  const DDRun* dd = P.dd + seg.dd_base;
-  for (u32 k = l; k < s.n_dd; k += 64) {
-    DDRun r = dd[k];
-    h += elem_hash(4, k, ((u64)r.key << 32) | r.len, r.excess);
+  const DDRun* dd = P.dd + seg.dd_base * DD_BLK;  // blocks in directory order = the flat RLE
+  const DDBlk* ddb = P.ddb + seg.dd_base;
+  for (u32 lb = 0, k0 = 0; lb < s.n_ddb; lb++) {
+    DDBlk B = w.ldT(ddb + lb);
+    if (l < B.cnt) {
+      DDRun r = dd[(u64)B.phys * DD_BLK + l];
+      h += elem_hash(4, k0 + l, ((u64)r.key << 32) | r.len, r.excess);
+    }
+    k0 += B.cnt;
   }
   const TxnRec* tx = P.txns + seg.txn_base;
   const u32* par = P.parents + seg.par_base;

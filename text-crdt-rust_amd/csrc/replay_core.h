@@ -54,8 +54,9 @@ enum : u32 {
   // DocState, field for field (struct order, 20 dwords)
   S_BASE = 40,
   S_STATUS = 40, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
-  S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES, S_GEN_DONE,
+  S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES, S_GEN_DONE, S_N_DDB,
   S_PROF0, S_PROF1, S_PROF2, S_PROF3,  // -DCRDT_PROF: cycles in typing / general / delete / insert paths
+  K_FR = 63,                            // frontier capacity
   // leaf cache bookkeeping
   C_LEAF = 64, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
@@ -67,10 +68,11 @@ enum : u32 {
   T_AG_ID, T_AG_BASE, T_AG_CNT, T_AG_CAP,
   T_AGL_KEY, T_AGL_ORDER, T_AGL_LEN,
   T_RB_BASE,
-  N_SLOTS
+  P_DDB,  // (2 slots) double-delete block directory
+  N_SLOTS = P_DDB + 2
 };
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
-static_assert(S_PROF3 < 64, "DocState lives in the first context register");
+static_assert(S_PROF3 < K_FR, "DocState lives in the first context register");
 static_assert(N_SLOTS <= 128, "two context registers");
 
 template <class W, int L>
@@ -105,6 +107,7 @@ struct Replayer {
   CRDT_HD ARun* arun() const { return ptr<ARun>(P_ARUN); }
   CRDT_HD DelRun* dels() const { return ptr<DelRun>(P_DELS); }
   CRDT_HD DDRun* dd() const { return ptr<DDRun>(P_DD); }
+  CRDT_HD DDBlk* ddb() const { return ptr<DDBlk>(P_DDB); }
   CRDT_HD TxnRec* txns() const { return ptr<TxnRec>(P_TXNS); }
   CRDT_HD u32* par() const { return ptr<u32>(P_PAR); }
   CRDT_HD u32* fr() const { return ptr<u32>(P_FR); }
@@ -125,7 +128,8 @@ struct Replayer {
     pset(P_CWO, P.cwo + sg.cwo_base);
     pset(P_ARUN, P.arun + sg.arun_base);
     pset(P_DELS, P.dels + sg.del_base);
-    pset(P_DD, P.dd + sg.dd_base);
+    pset(P_DD, P.dd + sg.dd_base * (u64)DD_BLK);
+    pset(P_DDB, P.ddb + sg.dd_base);
     pset(P_TXNS, P.txns + sg.txn_base);
     pset(P_PAR, P.parents + sg.par_base);
     pset(P_FR, P.frontier + sg.fr_base);
@@ -141,6 +145,7 @@ struct Replayer {
     p(K_DD, sg.dd_cap);
     p(K_PAR, sg.par_cap);
     p(K_RECN, sg.rec_n);
+    p(K_FR, sg.fr_cap);
     w.x_load_state(P.st + d, S_BASE);
     p(C_LEAF, INVALID);
     p(C_N, 0);
@@ -182,6 +187,7 @@ struct Replayer {
     p(S_CAP_NEED, 0);
     p(S_N_ENTRIES, 0);
     p(S_GEN_DONE, 0);
+    p(S_N_DDB, 0);
     w.zero_leaf(leafp(0), L);
     w.st(dl(), 0u);
     w.st(dv(), 0u);
@@ -685,63 +691,113 @@ struct Replayer {
     w.st_del(dels() + n, DelRun{key, target, len});
     p(S_N_DEL, n + 1);
   }
-  // double_delete.rs:41-107 increment_delete_range (rare path; scalar)
-  CRDT_HD bool dd_insert_at(u32 idx, DDRun r) {
-    u32 n = g(S_N_DD);
-    if (n + 1 > g(K_DD)) return false;
-    DDRun* b = dd();
-    for (u32 k = n; k > idx; k--) w.st_dd(b + k, w.ld_dd(b + k - 1));
-    w.st_dd(b + idx, r);
-    p(S_N_DD, n + 1);
+  // ---- double_deletes: an RLE of DDRun in 64-entry blocks (crdt_types.h DDBlk).  A position is
+  // (logical block, index); (n_ddb, 0) is the end.
+  struct DDPos { u32 lb, i; };
+  CRDT_HD u32 dd_nb() const { return g(S_N_DDB); }
+  CRDT_HD u32 dd_cnt(u32 lb) const { return w.ld(&ddb()[lb].cnt); }
+  CRDT_HD DDRun* dd_ptr(DDPos q) const { return dd() + (u64)w.ld(&ddb()[q.lb].phys) * DD_BLK + q.i; }
+  CRDT_HD DDRun dd_get(DDPos q) const { return w.ld_dd(dd_ptr(q)); }
+  CRDT_HD DDPos dd_next(DDPos q) const { return q.i + 1u < dd_cnt(q.lb) ? DDPos{q.lb, q.i + 1u} : DDPos{q.lb + 1u, 0u}; }
+  CRDT_HD DDPos dd_prev(DDPos q) const {  // q is not the first position
+    if (q.i) return DDPos{q.lb, q.i - 1u};
+    return DDPos{q.lb - 1u, dd_cnt(q.lb - 1u) - 1u};
+  }
+  // the position after the last entry with key <= x (entries are sorted by key)
+  CRDT_HD DDPos dd_upper(u32 x) const {
+    u32 nb = dd_nb();
+    i32 lb = nb ? w.search_first(ddb(), nb, x) : -1;
+    if (lb < 0) return DDPos{0u, 0u};
+    DDBlk B = w.ld_ddblk(ddb() + lb);
+    u32 k = w.dd_count_le(dd() + (u64)B.phys * DD_BLK, B.cnt, x);  // >= 1: first <= x
+    return k < B.cnt ? DDPos{(u32)lb, k} : DDPos{(u32)lb + 1u, 0u};
+  }
+  // Insert r before position q (Vec::insert); q becomes r's position.  A full block splits
+  // first: its upper 32 entries move to a new physical block linked right after it.
+  CRDT_HD bool dd_insert(DDPos& q, DDRun r) {
+    u32 nb = dd_nb();
+    if (nb == 0) {
+      if (g(K_DD) == 0) return false;
+      w.st_dd(dd(), r);
+      w.st_ddblk(ddb(), DDBlk{0u, r.key, 1u, 0u});
+      p(S_N_DDB, 1u);
+      inc(S_N_DD);
+      q = DDPos{0u, 0u};
+      return true;
+    }
+    if (q.lb >= nb) q = DDPos{nb - 1u, dd_cnt(nb - 1u)};  // the end: append to the last block
+    DDBlk B = w.ld_ddblk(ddb() + q.lb);
+    if (B.cnt == DD_BLK) {
+      if (nb >= g(K_DD)) return false;
+      u32 np = nb;  // physical blocks are allocated in order
+      u32 first2 = w.dd_split(dd() + (u64)B.phys * DD_BLK, dd() + (u64)np * DD_BLK);
+      w.ddb_insert(ddb(), nb, q.lb + 1u, DDBlk{np, first2, DD_BLK / 2u, 0u});
+      w.st(&ddb()[q.lb].cnt, DD_BLK / 2u);
+      p(S_N_DDB, nb + 1u);
+      if (q.i > DD_BLK / 2u) { q.lb += 1u; q.i -= DD_BLK / 2u; B = DDBlk{np, first2, DD_BLK / 2u, 0u}; }
+      else B.cnt = DD_BLK / 2u;
+    }
+    w.dd_block_insert(dd() + (u64)B.phys * DD_BLK, B.cnt, q.i, r);
+    w.st(&ddb()[q.lb].cnt, B.cnt + 1u);
+    if (q.i == 0u) w.st(&ddb()[q.lb].first, r.key);
+    inc(S_N_DD);
     return true;
   }
+  // double_delete.rs:41-107 increment_delete_range (on the blocked RLE; same steps as the
+  // reference's flat Vec: `idx` is a block position, Vec::insert is dd_insert)
   CRDT_HD bool increment_delete_range(u32 base, u32 len) {
-    DDRun* b = dd();
     DDRun next{base, len, 1};
-    i32 k = w.search_dd(b, g(S_N_DD), base);
-    u32 idx;
-    if (k >= 0) idx = (u32)k;
-    else {  // insertion point: first entry with key > base
-      idx = 0;
-      while (idx < g(S_N_DD) && w.ld_dd(b + idx).key <= base) idx++;
+    // the entry containing base (Rle::search), else the first entry with key > base
+    DDPos idx = dd_upper(base);
+    if (idx.lb | idx.i) {
+      DDPos q = dd_prev(idx);
+      DDRun e = dd_get(q);
+      if (base - e.key < e.len) idx = q;
     }
     while (true) {
-      if (idx == g(S_N_DD) || w.ld_dd(b + idx).key > base) {  // quirk Q9 (double_delete.rs:52)
+      bool end = idx.lb >= dd_nb();
+      DDRun cur = end ? DDRun{0, 0, 0} : dd_get(idx);
+      if (end || cur.key > base) {  // quirk Q9 (double_delete.rs:52)
         DDRun here = next;
         bool done_here;
-        if (idx < g(S_N_DD) && next.key + next.len > w.ld_dd(b + idx).key) {
-          u32 at = w.ld_dd(b + idx).key - here.key;
+        if (!end && next.key + next.len > cur.key) {
+          u32 at = cur.key - here.key;
           next = DDRun{here.key + at, here.len - at, here.excess};
           here.len = at;
           done_here = false;
         } else done_here = true;
         bool app = false;
-        if (idx >= 1) {
-          DDRun q = w.ld_dd(b + idx - 1);
-          if (here.key == q.key + q.len && here.excess == q.excess) { w.st(&b[idx - 1].len, q.len + here.len); app = true; }
+        if (idx.lb | idx.i) {
+          DDPos q = dd_prev(idx);
+          DDRun qq = dd_get(q);
+          if (here.key == qq.key + qq.len && here.excess == qq.excess) { w.st(&dd_ptr(q)->len, qq.len + here.len); app = true; }
         }
-        if (!app) { if (!dd_insert_at(idx, here)) return false; idx++; }
+        if (!app) {
+          if (!dd_insert(idx, here)) return false;
+          idx = dd_next(idx);
+        }
         if (done_here) break;
       }
-      DDRun e = w.ld_dd(b + idx);
+      DDRun e = dd_get(idx);
       if (e.key < next.key) {
         u32 at = next.key - e.key;
         DDRun rm{e.key + at, e.len - at, e.excess};
-        w.st(&b[idx].len, at);
-        idx++;
-        if (!dd_insert_at(idx, rm)) return false;
+        w.st(&dd_ptr(idx)->len, at);
+        idx = dd_next(idx);
+        if (!dd_insert(idx, rm)) return false;
       }
-      DDRun e2 = w.ld_dd(b + idx);
+      DDRun e2 = dd_get(idx);
       if (e2.len <= next.len) {
-        w.st(&b[idx].excess, e2.excess + 1);
+        w.st(&dd_ptr(idx)->excess, e2.excess + 1);
         next.key += e2.len;
         next.len -= e2.len;
         if (next.len == 0) break;
-        idx++;
+        idx = dd_next(idx);
       } else {
         DDRun rm{e2.key + next.len, e2.len - next.len, e2.excess};
-        w.st_dd(b + idx, DDRun{e2.key, next.len, e2.excess + 1});
-        if (!dd_insert_at(idx + 1, rm)) return false;
+        w.st_dd(dd_ptr(idx), DDRun{e2.key, next.len, e2.excess + 1});
+        DDPos after = dd_next(idx);
+        if (!dd_insert(after, rm)) return false;
         break;
       }
     }
@@ -780,7 +836,7 @@ struct Replayer {
             m++;
           }
         }
-        if (m + 1 > FRONTIER_CAP) return ST_CAPACITY;
+        if (m + 1 > g(K_FR)) return ST_CAPACITY;  // (fits() reserved room for nfr + 1 heads)
         if (m == 0) nf0 = last;
         else w.st(f + m, last);
         p(S_N_FR, m + 1);
@@ -827,8 +883,8 @@ struct Replayer {
 
   // ------------------------------------------------------------------ txn application
   // Capacity needed by a txn (checked before any mutation, so a capacity stop is resumable at
-  // this txn).  Every block but the first holds >= 32 slots, so blk_cap = leaf_cap/32 + 2 and
-  // leaf_cap <= 32*(MAX_GROUPS-1) (host-enforced) bound blocks and root groups as well.
+  // this txn).  Every block but the first holds >= 32 slots, so blk_cap = leaf_cap/32 + 2 bounds
+  // the blocks and the root groups as well (the host sizes the LDS root to blk_cap groups).
   // On failure S_CAP_NEED records which table (bit) must grow.
   CRDT_HD bool fits(bool remote, u32 agent, u32 n_ops, u32 n_dels, u32 txn_len, u32 n_parents) {
     // room = cap - count (count <= cap always holds), compared in 32 bits
@@ -838,10 +894,12 @@ struct Replayer {
     if (g(K_DEL) - g(S_N_DEL) < n_dels) need |= 4u;
     if (g(K_PAR) - g(S_N_PAR) < (remote ? n_parents : g(S_N_FR))) need |= 8u;
     if (g(K_MAP) - g(S_NEXT_ORDER) < txn_len) need |= 16u;
+    if (remote && g(K_FR) <= g(S_N_FR)) need |= 128u;  // a remote txn leaves <= nfr + 1 heads
     // double deletes (remote only): one txn adds at most 3 entries per existing entry it overlaps
-    // plus 2 per increment_delete_range call (<= one per deleted item)
+    // plus 2 per increment_delete_range call (<= one per deleted item); every block but the
+    // first holds >= 32 entries, so E entries need <= E/32 + 1 blocks
     u32 ndd = g(S_N_DD);
-    if (remote && n_dels && (u64)g(K_DD) - ndd < 3ull * ndd + 2ull * txn_len + 2ull) need |= 64u;
+    if (remote && n_dels && (4ull * ndd + 2ull * txn_len + 2ull) / 32ull + 2ull > (u64)g(K_DD)) need |= 64u;
     use_agent(agent);
     if (g(T_AG_CAP) == g(T_AG_CNT)) need |= 32u;
     p(S_CAP_NEED, need);

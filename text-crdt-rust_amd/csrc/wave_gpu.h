@@ -2,8 +2,8 @@
 //
 // One wavefront owns one document.  Lane-parallel state held in VGPRs:
 //   * the leaf cache: lane i < L holds entry i of the cached leaf (4 VGPRs: order, ol, orr, len);
-//   * the directory root: lane g of register r holds group 64r+g (block id, slot count, visible
-//     count), up to 4 registers = 256 groups = 16384 leaves per document.
+//   * the directory root in LDS: group g = (block id, slot count, visible count), a per-launch
+//     number of groups per wave (crdt_types.h ROOT_CAP_*).
 // Cross-lane steps use DPP row_shr / row_bcast scans (GFX9 form) and ds_bpermute shuffles;
 // uniform values are pulled to SGPRs with readfirstlane / readlane.
 #pragma once
@@ -68,11 +68,12 @@ struct WaveGPU {
   u32 eo = 0, el = 0, er = 0;
   i32 en = 0;
   // ---------------------------------------------------------------- root level (LDS)
-  // This wave's slice of the kernel's LDS: blk[MAX_GROUPS], cnt[MAX_GROUPS], vis[MAX_GROUPS]
-  // (structure of arrays: lane-parallel sweeps are bank-conflict free).  Kept out of VGPRs so
-  // that no register is ever indexed by a run-time group number.
+  // This wave's slice of the kernel's LDS: blk[rcap], cnt[rcap], vis[rcap] (structure of
+  // arrays: lane-parallel sweeps are bank-conflict free).  Kept out of VGPRs so that no register
+  // is ever indexed by a run-time group number.
   typedef __attribute__((address_space(3))) u32 lds_u32;  // ds_read/ds_write, never flat
   lds_u32* rt = nullptr;
+  u32 rcap = 0;
 
   // ---- scalar memory helpers (every lane touches the same address: uniform results, and a
   //      store is then visible to every lane's later loads by per-thread program order)
@@ -160,7 +161,67 @@ struct WaveGPU {
   __device__ __forceinline__ static u32 rlen(const TxnRec& r) { return r.len; }
   __device__ __forceinline__ i32 search_arun(const ARun* b, u32 n, u32 x) const { return search(b, n, x); }
   __device__ __forceinline__ i32 search_cwo(const CwoRun* b, u32 n, u32 x) const { return search(b, n, x); }
-  __device__ __forceinline__ i32 search_dd(const DDRun* b, u32 n, u32 x) const { return search(b, n, x); }
+  // ---- double-delete blocks (replay_core.h dd_*)
+  __device__ __forceinline__ DDBlk ld_ddblk(const DDBlk* p) const { return ldT(p); }
+  __device__ __forceinline__ void st_ddblk(DDBlk* p, const DDBlk& v) const { stT(p, v); }
+  // last block with first key <= x, or -1 (64-ary search, as `search`)
+  __device__ __forceinline__ i32 search_first(const DDBlk* b, u32 n, u32 x) const {
+    u32 lo = 0, hi = n;
+    u32 l = lane_id();
+    while (hi - lo > 64) {
+      u32 step = (hi - lo + 63) / 64;
+      u32 idx = lo + l * step;
+      u32 key = b[idx < hi ? idx : hi - 1].first;
+      u64 m = ballot(idx < hi && key <= x);
+      if (m == 0) return -1;
+      lo = lo + (63 - __builtin_clzll(m)) * step;
+      u32 nh = lo + step;
+      hi = nh < hi ? nh : hi;
+    }
+    u32 idx = lo + l;
+    u32 key = b[idx < hi ? idx : hi - 1].first;
+    u64 m = ballot(idx < hi && key <= x);
+    return m ? (i32)(lo + (63 - __builtin_clzll(m))) : -1;
+  }
+  // entries of one block (cnt >= 1) with key <= x
+  __device__ __forceinline__ u32 dd_count_le(const DDRun* blk, u32 cnt, u32 x) const {
+    u32 l = lane_id();
+    u32 key = blk[l < cnt ? l : 0u].key;
+    return (u32)__popcll(ballot(l < cnt && key <= x));
+  }
+  // entries [32, 64) of a full block move to [0, 32) of dst; returns dst's first key
+  __device__ __forceinline__ u32 dd_split(const DDRun* src, DDRun* dst) const {
+    u32 l = lane_id();
+    const u32* s = (const u32*)(src + (l | 32u));
+    u32 a = s[0], b = s[1], c = s[2];
+    if (l >= 32u) {
+      u32* d = (u32*)(dst + (l - 32u));
+      d[0] = a; d[1] = b; d[2] = c;
+    }
+    return rdlane(a, 32);
+  }
+  // Vec::insert at i of a block with cnt < 64 entries: [i, cnt) move up one, r goes to i
+  __device__ __forceinline__ void dd_block_insert(DDRun* blk, u32 cnt, u32 i, const DDRun& r) const {
+    u32 l = lane_id();
+    const u32* s = (const u32*)(blk + (l ? l - 1u : 0u));
+    u32 a = s[0], b = s[1], c = s[2];
+    bool me = l == i;
+    if (l >= i && l <= cnt) {
+      u32* d = (u32*)(blk + l);
+      d[0] = me ? r.key : a; d[1] = me ? r.len : b; d[2] = me ? r.excess : c;
+    }
+  }
+  // directory insert at `at` of n blocks: [at, n) move up one (64-block chunks, top down: each
+  // chunk's loads complete before its stores, and no later chunk reads what it stores)
+  __device__ __forceinline__ void ddb_insert(DDBlk* b, u32 n, u32 at, const DDBlk& v) const {
+    u32 l = lane_id();
+    for (i32 r = (i32)(n & ~63u); r >= (i32)(at & ~63u); r -= 64) {
+      u32 i = (u32)r + l;
+      uint4 x = *(const uint4*)(b + (i > 0u && i <= n ? i - 1u : 0u));
+      if (i > at && i <= n) *(uint4*)(b + i) = x;
+    }
+    stT(b + at, v);
+  }
   __device__ __forceinline__ i32 search_txn(const TxnRec* b, u32 n, u32 x) const { return search(b, n, x); }
 
   // ---------------------------------------------------------------- leaf cache
@@ -397,48 +458,38 @@ struct WaveGPU {
     }
   }
 
-  // ---------------------------------------------------------------- directory root (VGPRs)
+  // ---------------------------------------------------------------- directory root (LDS)
+  // Group g of the root: rblk()[g], rcnt()[g], rvis()[g]; rcap groups per array (a multiple of
+  // 64, chosen per launch).  Sweeps go 64 groups at a time, one group per lane.
   __device__ __forceinline__ lds_u32* rblk() const { return rt; }
-  __device__ __forceinline__ lds_u32* rcnt() const { return rt + MAX_GROUPS; }
-  __device__ __forceinline__ lds_u32* rvis() const { return rt + 2 * MAX_GROUPS; }
+  __device__ __forceinline__ lds_u32* rcnt() const { return rt + rcap; }
+  __device__ __forceinline__ lds_u32* rvis() const { return rt + 2 * rcap; }
   __device__ __forceinline__ void root_init(u32 blk, u32 cnt, u32 vis) {
     rblk()[0] = blk;  // every lane stores the same value: no branch
     rcnt()[0] = cnt;
     rvis()[0] = vis;
   }
   __device__ __forceinline__ void root_load(const GroupRec* g, u32 ng) {
-    u32 l = lane_id();
-#pragma unroll
-    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
-      u32 i = r * 64 + l;
-      if (i < ng) {
-        uint4 x = *(const uint4*)(g + i);
-        rblk()[i] = x.x;
-        rcnt()[i] = x.y;
-        rvis()[i] = x.z;
-      }
+    for (u32 i = lane_id(); i < ng; i += 64) {
+      uint4 x = *(const uint4*)(g + i);
+      rblk()[i] = x.x;
+      rcnt()[i] = x.y;
+      rvis()[i] = x.z;
     }
   }
   __device__ __forceinline__ void root_store(GroupRec* g, u32 ng) const {
-    u32 l = lane_id();
-#pragma unroll
-    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
-      u32 i = r * 64 + l;
-      if (i < ng) *(uint4*)(g + i) = make_uint4(rblk()[i], rcnt()[i], rvis()[i], 0);
-    }
+    for (u32 i = lane_id(); i < ng; i += 64) *(uint4*)(g + i) = make_uint4(rblk()[i], rcnt()[i], rvis()[i], 0);
   }
   __device__ __forceinline__ u32 root_blk(u32 g) const { return uni(rblk()[g]); }
   __device__ __forceinline__ u32 root_cnt(u32 g) const { return uni(rcnt()[g]); }
   __device__ __forceinline__ u32 root_vis(u32 g) const { return uni(rvis()[g]); }
   __device__ __forceinline__ u32 root_find_blk(u32 ng, u32 blk) const {
     u32 l = lane_id();
-#pragma unroll
-    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
-      if (r * 64 >= ng) break;
-      u32 i = r * 64 + l;
-      u32 b = rblk()[i];  // i < MAX_GROUPS: always inside this wave's LDS slice
+    for (u32 r = 0; r < ng; r += 64) {
+      u32 i = r + l;
+      u32 b = rblk()[i];  // i < rcap (a multiple of 64): always inside this wave's LDS slice
       u64 m = ballot(i < ng && b == blk);
-      if (m) return r * 64 + __builtin_ctzll(m);
+      if (m) return r + (u32)__builtin_ctzll(m);
     }
     return INVALID;
   }
@@ -451,44 +502,35 @@ struct WaveGPU {
     rcnt()[g] = cnt;
     rvis()[g] = vis;
   }
-  // insert a group at index g, shifting [g, ng) up by one (read everything, then write)
+  // insert a group at index g, shifting [g, ng) up by one: 64-group chunks from the top down, each
+  // read completely before it is written (a chunk's lane 0 reads the top of the chunk below,
+  // which is written only afterwards)
   __device__ __forceinline__ void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
     u32 l = lane_id();
-    u32 b[MAX_GROUP_REGS], c[MAX_GROUP_REGS], v[MAX_GROUP_REGS];
-#pragma unroll
-    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
-      u32 i = r * 64 + l;
-      u32 j = i - 1;
-      u32 jj = j & (MAX_GROUPS - 1);
-      b[r] = rblk()[jj];
-      c[r] = rcnt()[jj];
-      v[r] = rvis()[jj];
+    for (i32 r = (i32)(ng & ~63u); r >= (i32)(g & ~63u); r -= 64) {
+      u32 i = (u32)r + l;
+      u32 jj = i > 0u ? i - 1u : 0u;
+      u32 b = rblk()[jj], c = rcnt()[jj], v = rvis()[jj];
+      __builtin_amdgcn_wave_barrier();
+      if (i > g && i <= ng) { rblk()[i] = b; rcnt()[i] = c; rvis()[i] = v; }
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
-      u32 i = r * 64 + l;
-      if (i > g && i <= ng) { rblk()[i] = b[r]; rcnt()[i] = c[r]; rvis()[i] = v[r]; }
-    }
-    __builtin_amdgcn_wave_barrier();
     root_set(g, blk, cnt, vis);
   }
   // first group whose cumulative visible count exceeds pos
   __device__ __forceinline__ bool root_find_pos(u32 ng, u32 pos, u32& g, u32& base) const {
     u32 l = lane_id();
     u32 carry = 0;
-#pragma unroll
-    for (u32 r = 0; r < MAX_GROUP_REGS; r++) {
-      if (r * 64 >= ng) break;
-      u32 i = r * 64 + l;
+    for (u32 r = 0; r < ng; r += 64) {
+      u32 i = r + l;
       bool valid = i < ng;
       u32 xv = rvis()[i];
       u32 x = valid ? xv : 0u;
       u32 incl = wave_incl_scan(x) + carry;
-      u32 nvalid = ng - r * 64 < 64 ? ng - r * 64 : 64;
+      u32 nvalid = ng - r < 64 ? ng - r : 64;
       u32 k = __popcll(ballot(valid && incl <= pos));
       if (k < nvalid) {
-        g = r * 64 + k;
+        g = r + k;
         base = rdlane(incl, k) - rdlane(x, k);
         return true;
       }
