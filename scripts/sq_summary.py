@@ -1,0 +1,50 @@
+"""Summarise the SQ PMC passes of ONE clean k_replay launch (scripts/gpu_pmc_all.sh) into a
+profiles/ JSON: counter totals (last k_replay dispatch of each pass), instructions per op and per
+wave, and issue utilisation.
+
+usage: python scripts/sq_summary.py OUT.json DOCS [OPS_PER_DOC] [TAG]
+SQ counters on gfx950 count per wave-instruction; SQ_WAVE_CYCLES / SQ_BUSY_CYCLES are in the SQ
+clock.  WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES (MI355X_MICROARCH.md, PMC
+slots)."""
+import csv
+import glob
+import json
+import sys
+
+out, docs = sys.argv[1], int(sys.argv[2])
+ops_doc = int(sys.argv[3]) if len(sys.argv) > 3 else 259778
+tag = sys.argv[4] if len(sys.argv) > 4 else ""
+agg, meta = {}, {}
+for f in sorted(glob.glob(f"gpurun_out/pmc[123]{tag}/**/*counter_collection.csv", recursive=True)):
+    rows = [r for r in csv.DictReader(open(f)) if "k_replay" in r.get("Kernel_Name", "")]
+    last = max(int(r["Dispatch_Id"]) for r in rows)
+    for r in rows:
+        if int(r["Dispatch_Id"]) == last:
+            agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+            meta = {"vgpr": int(r["VGPR_Count"]), "sgpr": int(r["SGPR_Count"]), "lds_block": int(r["LDS_Block_Size"]),
+                    "kernel_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])}
+ops = docs * ops_doc
+waves = agg.get("SQ_WAVES", docs)
+inst = {k: agg[k] for k in agg if k.startswith("SQ_INSTS_")}
+total_inst = sum(agg.get(k, 0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                                         "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_FLAT"))
+wc = agg.get("SQ_WAVE_CYCLES", 0)
+res = {
+    "kernel": "k_replay<32>", "docs": docs, "ops_per_doc": ops_doc, "workload": "config 2: automerge-paper remote, one clean launch",
+    "launch": meta, "counters": agg,
+    "per_op": {k.replace("SQ_INSTS_", "").lower(): v / ops for k, v in inst.items()},
+    "instructions_per_op": total_inst / ops,
+    "ratios": {
+        "active_inst_any / wave_cycles": agg.get("SQ_ACTIVE_INST_ANY", 0) / wc if wc else None,
+        "wait_any / wave_cycles": agg.get("SQ_WAIT_ANY", 0) / wc if wc else None,
+        "wait_inst_any / wave_cycles": agg.get("SQ_WAIT_INST_ANY", 0) / wc if wc else None,
+        "active_inst_sca / wave_cycles": agg.get("SQ_ACTIVE_INST_SCA", 0) / wc if wc else None,
+        "active_inst_valu / wave_cycles": agg.get("SQ_ACTIVE_INST_VALU", 0) / wc if wc else None,
+        "salu_insts / all_insts": agg.get("SQ_INSTS_SALU", 0) / total_inst if total_inst else None,
+        "valu_insts / all_insts": agg.get("SQ_INSTS_VALU", 0) / total_inst if total_inst else None,
+        "wave_cycles_per_wave": wc / waves if waves else None,
+        "busy_cycles": agg.get("SQ_BUSY_CYCLES"),
+    },
+}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))

@@ -150,7 +150,29 @@ struct WaveCPU {
     for (u32 i = 0; i < n_ahead; i++) qb[i] = p_ahead[i];
   }
   Rec rec_get(u32 k) const { return rb[k]; }
-  u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 ow1, u32 ow3, u32& total) const {
+  u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3, u32& total) const {
+    if (compact) {
+      u32 n = 1;
+      total = remote ? rc_len(rb[b0]) : rb[b0].w3;
+      for (u32 j = b0 + 1; j < nv; j++) {
+        const Rec &r = rb[j], &p = rb[j - 1];
+        bool ok;
+        u32 hl;
+        if (remote) {
+          hl = rc_len(r);
+          u32 ra = r.w3 == 0xFFFFFFFFu ? 0xFFFFu : agent;
+          ok = (r.w0 & RC_HDR_MASK) == ((REC_RC << 28) | agent) && hl != 0 && r.w1 == p.w1 + rc_len(p) &&
+               r.w2 == r.w1 - 1u && r.w3 == ow3 && (agent | (ra << 16)) == ow1;
+        } else {
+          hl = r.w3;
+          ok = r.w0 == ((REC_LC << 28) | agent) && r.w2 == 0u && r.w3 - 1u < 0xFFFFu && r.w1 == p.w1 + p.w3;
+        }
+        if (!ok) break;
+        n++;
+        total += hl;
+      }
+      return n;
+    }
     u32 per = remote ? 3u : 2u;
     u32 n = 1;
     total = rb[b0].w3;
@@ -174,7 +196,18 @@ struct WaveCPU {
     return n;
   }
 
-  u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 delta) const {
+  u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+    if (compact) {
+      u32 n = 1;
+      for (u32 j = b0 + 1; j < nv; j++) {
+        const Rec &r = rb[j], &p = rb[j - 1];
+        bool ok = remote ? (r.w0 == ((REC_RC << 28) | (1u << 27) | (1u << 16) | agent) && r.w1 == p.w1 + 1u && r.w2 == p.w2 + delta)
+                         : (r.w0 == ((REC_LC << 28) | agent) && r.w2 == 1u && r.w3 == 0u && r.w1 == p.w1 + delta);
+        if (!ok) break;
+        n++;
+      }
+      return n;
+    }
     u32 per = remote ? 3u : 2u;
     u32 n = 1;
     for (u32 j = b0 + per; j + per <= nv; j += per) {

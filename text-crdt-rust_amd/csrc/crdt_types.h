@@ -96,7 +96,8 @@ struct GroupRec { u32 blk, cnt, vis, pad; };   // persisted root level of the di
 // ---------------------------------------------------------------------------------------------
 // Op record stream (16 B records, per document, in causal order)
 // ---------------------------------------------------------------------------------------------
-enum : u32 { REC_LTXN = 1, REC_LOP = 2, REC_RTXN = 3, REC_RINS = 4, REC_RDEL = 5, REC_RPARENT = 6, REC_GEN = 7 };
+enum : u32 { REC_LTXN = 1, REC_LOP = 2, REC_RTXN = 3, REC_RINS = 4, REC_RDEL = 5, REC_RPARENT = 6, REC_GEN = 7,
+             REC_RC = 8, REC_LC = 9 };
 struct Rec { u32 w0, w1, w2, w3; };
 // LTXN    w0 = kind<<28 | n_ops         w1 = agent                  w2 = sum(del) w3 = txn_len
 // LOP     w0 = kind<<28                 w1 = pos                    w2 = del   w3 = ins
@@ -108,7 +109,32 @@ struct Rec { u32 w0, w1, w2, w3; };
 // GEN     w0 = kind<<28                 w1 = agent                  w2 = n_ops w3 = seed
 // (remote ops follow their RTXN, then the txn's RPARENT records; a GEN record expands on the
 //  device into n_ops local txns of one LocalOp each, see gen_op)
+// Compact one-record txns (the common shape of real traces: 16 B per op instead of 48 / 32):
+// RC      w0 = kind<<28 | del<<27 | len<<16 (11 b, 1..2047) | author
+//                                       w1 = seq   w2 = ins: origin_left seq, del: target seq
+//                                                  w3 = ins: origin_right seq
+//         one RemoteOp; its origins / target are the author's items (a seq of 0xFFFFFFFF names
+//         ROOT); the one parent is (author, seq - 1)
+// LC      w0 = kind<<28 | agent (16 b)  w1 = pos   w2 = del   w3 = ins   (one LocalOp)
 CRDT_HD u32 rec_kind(const Rec& r) { return r.w0 >> 28; }
+constexpr u32 RC_HDR_MASK = 0xF800FFFFu;  // kind | del | author (not len)
+CRDT_HD u32 rc_len(const Rec& r) { return (r.w0 >> 16) & 0x7FFu; }
+// the general records a compact txn stands for (header, op, parent)
+CRDT_HD void expand_rc(const Rec r, Rec& h, Rec& o, Rec& pr) {  // (r by value: h may alias it)
+  u32 a = r.w0 & 0xFFFFu, len = rc_len(r);
+  h = Rec{(REC_RTXN << 28) | 1u, a | (1u << 16), r.w1, len};
+  if ((r.w0 >> 27) & 1u) {
+    o = Rec{(REC_RDEL << 28) | len, a, r.w2, 0u};
+  } else {
+    u32 la = r.w2 == 0xFFFFFFFFu ? ROOT_AGENT : a, ra = r.w3 == 0xFFFFFFFFu ? ROOT_AGENT : a;
+    o = Rec{(REC_RINS << 28) | len, la | (ra << 16), r.w2, r.w3};
+  }
+  pr = Rec{REC_RPARENT << 28, a, r.w1 - 1u, 0u};
+}
+CRDT_HD void expand_lc(const Rec r, Rec& h, Rec& o) {
+  h = Rec{(REC_LTXN << 28) | 1u, r.w0 & 0xFFFFu, r.w2, r.w2 + r.w3};
+  o = Rec{REC_LOP << 28, r.w1, r.w2, r.w3};
+}
 
 CRDT_HD u64 mix64(u64 z) {  // splitmix64 finaliser
   z += 0x9E3779B97F4A7C15ull;

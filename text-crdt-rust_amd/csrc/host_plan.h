@@ -110,10 +110,15 @@ inline void encode_local_txn(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, 
   for (u32 k = 0; k < nops; k++) { span += (u64)ops3[3 * k + 1] + ops3[3 * k + 2]; dels += ops3[3 * k + 1]; }
   u32 span32 = span > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)span;
   u32 dels32 = dels > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)dels;
-  out.push_back(Rec{(REC_LTXN << 28) | (nops & 0x0FFFFFFFu), agent, dels32, span32});
-  for (u32 k = 0; k < nops; k++) {
-    out.push_back(Rec{REC_LOP << 28, ops3[3 * k], ops3[3 * k + 1], ops3[3 * k + 2]});
-    nd.local_del += ops3[3 * k + 1];
+  if (nops == 1 && agent <= 0xFFFFu && span <= 0xFFFFFFFFull) {  // one LocalOp: one compact record
+    out.push_back(Rec{(REC_LC << 28) | agent, ops3[0], ops3[1], ops3[2]});
+    nd.local_del += ops3[1];
+  } else {
+    out.push_back(Rec{(REC_LTXN << 28) | (nops & 0x0FFFFFFFu), agent, dels32, span32});
+    for (u32 k = 0; k < nops; k++) {
+      out.push_back(Rec{REC_LOP << 28, ops3[3 * k], ops3[3 * k + 1], ops3[3 * k + 2]});
+      nd.local_del += ops3[3 * k + 1];
+    }
   }
   nd.n_txn++;
   nd.n_ltxn++;
@@ -143,6 +148,34 @@ inline void encode_remote(std::vector<Rec>& out, StreamNeeds& nd, AgentTable& at
       tl += len;
     }
     u32 tl32 = tl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)tl;
+    // the common shape -- one op on the author's own items (or ROOT), the author's previous txn
+    // as the only parent -- is one compact record (crdt_types.h RC)
+    if (t.n_ops == 1 && t.n_parents == 1 && author < 0xFFFEu && t.seq >= 1 && res(t.parents[0]) == author &&
+        t.parents[1] == t.seq - 1) {
+      const u32* o = t.ops;
+      u32 len = o[5];
+      auto org = [&](u32 ni, u32 seq, u32& enc) -> bool {  // author's item or ROOT
+        u32 a = res(ni);
+        if (a == ROOT_AGENT) { enc = 0xFFFFFFFFu; return true; }
+        enc = seq;
+        return a == author && seq != 0xFFFFFFFFu;
+      };
+      u32 e2 = 0, e3 = 0;
+      bool ok = len >= 1 && len <= 0x7FFu;
+      if (ok && o[0] == 0) ok = org(o[1], o[2], e2) && org(o[3], o[4], e3);
+      else if (ok) ok = res(o[1]) == author && o[2] != 0xFFFFFFFFu && (e2 = o[2], true);
+      if (ok) {
+        out.push_back(Rec{(REC_RC << 28) | ((o[0] ? 1u : 0u) << 27) | (len << 16) | author, t.seq, e2, e3});
+        if (o[0]) nd.remote_del_ops++;
+        nd.n_txn++;
+        nd.n_rtxn++;
+        nd.n_ops += 1;
+        nd.orders += tl;
+        nd.remote_parents += 1;
+        nd.agent_txn(author);
+        continue;
+      }
+    }
     out.push_back(Rec{(REC_RTXN << 28) | ((zero ? 1u : 0u) << 27) | (t.n_ops & 0x07FFFFFFu),
                       (author & 0xFFFFu) | ((t.n_parents & 0xFFFFu) << 16), t.seq, tl32});
     for (u32 k = 0; k < t.n_ops; k++) {

@@ -83,6 +83,24 @@ struct Replayer {
   u32 pre = 0;
   Span pre_item{0, 0, 0, 0};
   Cursor pre_c{0, 0, 0};
+  // record format of the txn fast_txn is working on: compact one-record txns (RC / LC) or the
+  // general header + ops (+ parents) form
+  u32 cpt = 0;
+  CRDT_HD u32 per_txn(u32 remote) const { return cpt ? 1u : (remote ? 3u : 2u); }
+  // the op record of the one-op txn at window slot b
+  CRDT_HD Rec op_at(u32 b, u32 remote) const {
+    Rec r = w.rec_get(cpt ? b : b + 1u);
+    if (!cpt) return r;
+    Rec h, o, pr;
+    if (remote) expand_rc(r, h, o, pr);
+    else expand_lc(r, h, o);
+    return o;
+  }
+  // the length of the one-op txn at window slot b
+  CRDT_HD u32 len_at(u32 b, u32 remote) const {
+    Rec r = w.rec_get(b);
+    return (cpt & remote) ? rc_len(r) : r.w3;  // (a typing / delete-run LC has del = 0 or ins = 0)
+  }
 #ifdef CRDT_PROF
   u32 prof_cat = 0;  // diagnostic: which fast path ran (0 typing, 2 delete, 3 insert)
 #endif
@@ -912,7 +930,9 @@ struct Replayer {
   // One txn: doc.rs:376-469 apply_local_txn (remote = false) or doc.rs:242-348
   // apply_remote_txn (remote = true).  Header at record `pos`; ops (then parents) follow.
   // gen: the txn comes from a GEN record; its single LocalOp is `gop` (no op record to read).
-  CRDT_HD i32 apply_txn(const Rec& h, u32 pos, bool remote, u32 gen, const Rec& gop) {
+  // inl: the txn's single op (and for a remote txn its single parent) are gop / gpar, not records
+  // after the header (a compact record, or a generated op)
+  CRDT_HD i32 apply_txn(const Rec& h, u32 pos, bool remote, u32 inl, const Rec& gop, const Rec& gpar) {
     u32 nops, agent, np = 0, seq, txn_len;
     if (!remote) {
       nops = h.w0 & 0x0FFFFFFFu;
@@ -955,7 +975,7 @@ struct Replayer {
       // ---------------------------------------------------------------- next op
       if (mode == M_FETCH) {
         if (k == nops) break;
-        Rec op = gen ? gop : rec(pos + 1 + k);
+        Rec op = inl ? gop : rec(pos + 1 + k);
         k++;
         if (!remote) {  // LocalOp: delete (visible range) first, then insert (doc.rs:386-465)
           lpos = op.w1;
@@ -1105,7 +1125,7 @@ struct Replayer {
     if (remote) {
       u32* pp = par() + g(S_N_PAR);
       for (u32 j = 0; j < np; j++) {
-        Rec pr = rec(pos + 1 + nops + j);
+        Rec pr = inl ? gpar : rec(pos + 1 + nops + j);
         if (rec_kind(pr) != REC_RPARENT) return ST_BAD_INPUT;
         u32 o;
         i32 st = id_to_order(pr.w1 & 0xFFFFu, pr.w2, o);
@@ -1165,17 +1185,17 @@ struct Replayer {
     u32 nt = 1u;
     total = remote ? (o.w0 & 0x0FFFFFFFu) : o.w3;
     if (!nv) return nt;
-    nt = w.typing_scan(b0, nv, remote, agent, ow1, o.w3, total);
-    u32 per = remote ? 3u : 2u, rn = rec_n();
+    nt = w.typing_scan(b0, nv, remote, cpt, agent, ow1, o.w3, total);
+    u32 per = per_txn(remote), rn = rec_n();
     u32 pos0 = g(T_RB_BASE) + b0;
     while ((pos0 + (nt + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
       u32 last = pos0 + (nt - 1u) * per;
       rec_window(last);
       nv = rn - last < 64u ? rn - last : 64u;
       u32 t2;
-      u32 n2 = w.typing_scan(0u, nv, remote, agent, ow1, o.w3, t2);
+      u32 n2 = w.typing_scan(0u, nv, remote, cpt, agent, ow1, o.w3, t2);
       if (n2 <= 1u) break;
-      total += t2 - w.rec_get(0u).w3;
+      total += t2 - len_at(0u, remote);
       nt += n2 - 1u;
     }
     return nt;
@@ -1191,7 +1211,7 @@ struct Replayer {
     set(idx, e);
     inc(S_N_ITEMS, total);
     fast_txn_commit(first, total);
-    return nt * (remote ? 3u : 2u);
+    return nt * per_txn(remote);
   }
   // Delete `l` items at offset `off` of visible entry idx of the cached leaf: mutate_entry
   // (mutations.rs:227-277) and insert_internal's prepend / shift (mutations.rs:84-146) without a
@@ -1296,7 +1316,7 @@ struct Replayer {
   // would (leaf_delete); the RLE tables, the order map and the txn log are updated once for the
   // run.  Returns records consumed (0: nothing applied).
   CRDT_HD u32 fast_deletes(u32 b0, u32 nv, u32 remote, u32 agent, u32 idx, u32 off, u32 l, u32 first, const Rec& o) {
-    u32 per = remote ? 3u : 2u;
+    u32 per = per_txn(remote);
     u32 t1 = w.cget_order(idx) + off;
     if (g(C_N) + 2u > (u32)L) {  // near-full leaf: does the first delete fit (leaf_delete's rule)?
       Span e = w.cget(idx);
@@ -1312,7 +1332,7 @@ struct Replayer {
     u32 key = g(T_AGL_KEY);
     u32 in_run = !remote || (((o.w1 & 0xFFFFu) == agent) & (o.w2 - key < g(T_AGL_LEN)));
     if ((l == 1u) & (b0 + 2u * per <= nv) & in_run) {
-      Rec o2 = w.rec_get(b0 + per + 1u);
+      Rec o2 = op_at(b0 + per, remote);
       u32 delta = remote ? o2.w2 - o.w2 : o2.w1 - o.w1;
       back = delta == 0xFFFFFFFFu;
       u32 fwd = delta == (remote ? 1u : 0u);
@@ -1322,7 +1342,7 @@ struct Replayer {
           u32 r2 = back ? o.w2 - key + 1u : key + g(T_AGL_LEN) - o.w2;
           room = room < r2 ? room : r2;
         }
-        k = w.delete_scan(b0, nv, remote, agent, delta);
+        k = w.delete_scan(b0, nv, remote, cpt, agent, delta);
         // the run may go on past the window: slide the window to its last txn and scan on
         u32 rn = rec_n();
         u32 pos0 = g(T_RB_BASE) + b0;
@@ -1330,7 +1350,7 @@ struct Replayer {
           u32 last = pos0 + (k - 1u) * per;
           rec_window(last);
           nv = rn - last < 64u ? rn - last : 64u;
-          u32 n2 = w.delete_scan(0u, nv, remote, agent, delta);
+          u32 n2 = w.delete_scan(0u, nv, remote, cpt, agent, delta);
           if (n2 <= 1u) break;
           k += n2 - 1u;
         }
@@ -1396,13 +1416,15 @@ struct Replayer {
   }
   // Returns the records consumed by a fast-path txn at `pos`, or 0 (use apply_txn).
   // gen: a txn expanded from a GEN record (header gh, op go; no record window, no runs).
+  // kind: the record kind at `pos` (RTXN / LTXN / RC / LC; LTXN for a generated op).
   CRDT_HD u32 fast_txn(u32 pos, u32 kind, u32 gen, const Rec& gh, const Rec& go) {
-    u32 remote = kind == REC_RTXN;
-    u32 per = remote ? 3u : 2u;
+    cpt = (kind == REC_RC) | (kind == REC_LC);
+    u32 remote = (kind == REC_RTXN) | (kind == REC_RC);
+    u32 per = per_txn(remote);
     u32 rn = rec_n();
     if (g(C_LEAF) == INVALID) return 0;
     u32 b0 = 0, nv = 0;
-    Rec h = gh, o = go;
+    Rec h = gh, o = go, pr{0, 0, 0, 0};
     if (!gen) {
       if (rn - pos < per) return 0;
       b0 = pos - g(T_RB_BASE);
@@ -1413,13 +1435,18 @@ struct Replayer {
       nv = rn - g(T_RB_BASE);
       nv = nv < 64u ? nv : 64u;
       h = w.rec_get(b0);
-      o = w.rec_get(b0 + 1u);
+      if (cpt) {
+        if (remote) expand_rc(h, h, o, pr);
+        else expand_lc(h, h, o);
+      } else {
+        o = w.rec_get(b0 + 1u);
+        if (remote) pr = w.rec_get(b0 + 2u);
+      }
     }
     u32 first = g(S_NEXT_ORDER);
     u32 agent, l, ins, ol = 0, orr = ROOT_ORDER;
     Cursor c;
     if (remote) {
-      Rec pr = w.rec_get(b0 + 2u);
       agent = h.w1 & 0xFFFFu;
       u32 seq = h.w2;
       l = o.w0 & 0x0FFFFFFFu;
@@ -1492,17 +1519,19 @@ struct Replayer {
       Rec h = rec(pos);
       u32 kind = rec_kind(h);
       u32 gen = kind == REC_GEN;
-      Rec gop{0, 0, 0, 0};
+      Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
+      u32 inl = 0;
       if (gen) {
         u32 done = g(S_GEN_DONE);
         if (done >= h.w2) { p(S_GEN_DONE, 0); pos += 1; continue; }
         gop = gen_op(h.w3, done, cur_len());
         h = Rec{(REC_LTXN << 28) | 1u, h.w1, gop.w2, gop.w2 + gop.w3};
         kind = REC_LTXN;
+        inl = 1;
       }
       i32 st;
       u32 consumed;
-      if (kind == REC_LTXN || kind == REC_RTXN) {
+      if (kind == REC_LTXN || kind == REC_RTXN || kind == REC_RC || kind == REC_LC) {
 #ifdef CRDT_PROF
         u64 t0 = w.clock();
 #endif
@@ -1520,10 +1549,12 @@ struct Replayer {
           else pos += fast;
           continue;
         }
-        bool remote = kind == REC_RTXN;
+        bool remote = kind == REC_RTXN || kind == REC_RC;
+        if (kind == REC_RC) { expand_rc(h, h, gop, gpar); inl = 1; }
+        if (kind == REC_LC) { expand_lc(h, h, gop); inl = 1; }
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
-        consumed = gen ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
-        st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, gen, gop) : ST_BAD_INPUT;
+        consumed = inl ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
+        st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, inl, gop, gpar) : ST_BAD_INPUT;
         pre = 0;
 #ifdef CRDT_PROF
         inc(S_PROF1, (u32)(w.clock() - t1));

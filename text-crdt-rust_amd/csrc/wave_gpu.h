@@ -393,8 +393,28 @@ struct WaveGPU {
   // seq + previous length; local: LTXN{1 op}, LOP insert at the previous pos + previous length.
   // The txn at b0 was checked by the caller.  Returns the run length in txns (>= 1) and the
   // total inserted length.  nv = valid records in the block.
-  __device__ __forceinline__ u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 ow1, u32 ow3, u32& total) const {
+  // compact: one record per txn (crdt_types.h RC / LC), lane k checks record k against record k-1.
+  __device__ __forceinline__ u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3,
+                                             u32& total) const {
     u32 l = lane_id();
+    if (compact) {
+      u32 p0 = shfl(rx, l - 1u), p1 = shfl(ry, l - 1u), p3 = shfl(rw, l - 1u);
+      bool ok;
+      u32 hl;
+      if (remote) {
+        hl = (rx >> 16) & 0x7FFu;
+        u32 ra = rw == 0xFFFFFFFFu ? 0xFFFFu : agent;  // origin_right's agent (ROOT or the author)
+        ok = (rx & RC_HDR_MASK) == ((REC_RC << 28) | agent) && hl != 0u && ry == p1 + ((p0 >> 16) & 0x7FFu) &&
+             rz == ry - 1u && rw == ow3 && (agent | (ra << 16)) == ow1;
+      } else {
+        hl = rw;
+        ok = rx == ((REC_LC << 28) | agent) && rz == 0u && rw - 1u < 0xFFFFu && ry == p1 + p3;
+      }
+      u64 stop = ballot(l > b0 && (!ok || l >= nv));
+      u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
+      total = wave_sum(l >= b0 && l < f ? hl : 0u);
+      return f - b0;
+    }
     u32 rel = l - b0;  // wraps below b0: those lanes are masked
     u32 per = remote ? 3u : 2u;
     u32 t = remote ? (rel * 43u) >> 7 : rel >> 1;  // rel / 3 exactly for rel < 64
@@ -425,8 +445,16 @@ struct WaveGPU {
   // seq + 1, RDEL of 1 item of `agent` at the previous target seq + delta, RPARENT (agent, seq-1);
   // local: LTXN{1 op} deleting 1 item at the previous pos + delta.  Returns the run length in
   // txns (>= 1; the txn at b0 was checked by the caller).
-  __device__ __forceinline__ u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 agent, u32 delta) const {
+  __device__ __forceinline__ u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
     u32 l = lane_id();
+    if (compact) {  // one record per txn: lane k against record k-1
+      u32 p1 = shfl(ry, l - 1u), p2 = shfl(rz, l - 1u);
+      bool ok = remote ? ((rx == ((REC_RC << 28) | (1u << 27) | (1u << 16) | agent)) && ry == p1 + 1u && rz == p2 + delta)
+                       : (rx == ((REC_LC << 28) | agent) && rz == 1u && rw == 0u && ry == p1 + delta);
+      u64 stop = ballot(l > b0 && (!ok || l >= nv));
+      u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
+      return f - b0;
+    }
     u32 rel = l - b0;
     u32 per = remote ? 3u : 2u;
     u32 t = remote ? (rel * 43u) >> 7 : rel >> 1;
