@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: CRDT ops remapped+merged per second on MI355X (BASELINE.json metric).
 
-Workload (BASELINE config 2): `--docs` (default 4096) independent copies of the
+Workload (BASELINE config 2): `--docs` (default 8192) independent copies of the
 automerge-paper trace per GPU, delivered as remote txns (apply_remote_txn path) with randomised
 client ids (agent name = hex(splitmix64(0xC0FFEE ^ doc))).  One step = reset all documents to
 ListCRDT::new(), replay every document's 259,778 remote ops (merge: (agent,seq)->order remap +
@@ -288,7 +288,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--docs", type=int, default=4096, help="documents per GPU")
+    ap.add_argument("--docs", type=int, default=8192, help="documents per GPU (8 waves per SIMD)")
     ap.add_argument("--trace", default="automerge-paper")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
@@ -338,6 +338,8 @@ def main():
     assert (st == 0).all(), np.unique(st)
     eng.publish_async()
     eng.sync()
+    eng.fit()  # capacities = what this stream uses (the timed replays need exactly that)
+    mem = eng.mem_bytes()
     lens = eng.lens()
     # query batch (device resident): positions spread over every document
     rng = np.random.default_rng(1234 + rank)
@@ -437,7 +439,7 @@ def main():
             "config": {"workload": f"config2: {n} docs/GPU x {args.trace} remote txns ({n_ops_doc} ops/doc), "
                                    f"replay+publish+{q} pos->loc & loc->pos queries/doc",
                        "docs_per_gpu": n, "ops_per_doc": n_ops_doc, "parallelism": f"doc-sharded x{world}",
-                       "waves_per_simd": n / SIMDS},
+                       "waves_per_simd": n / SIMDS, "hbm_bytes_per_doc": mem / n},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": measured_traffic(n),
                          "kernel": "k_replay<32>", "kernel_ms": rms, "alg_bytes_per_launch": alg_bytes,

@@ -184,6 +184,21 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
                 uint32_t* frontier);
 
 /* Raw per-document replay state (22 u32: status, resume point, table sizes, ...; debugging). */
+// Shrink every document's per-table capacities to what its staged stream used (call after a
+// crdt_run + publish of it; a later reset + crdt_run_async replays it in exactly that room).
+// Capacities grow again on the next stage.  (Host-side planning; no reference counterpart.)
+int crdt_fit(crdt_engine* e);
+// Device bytes the engine holds (per-document pools, staged records, content, text).
+uint64_t crdt_mem_bytes(const crdt_engine* e);
+// Config 1's per-op check: after txn t (of every listed document), ask pos_to_loc(probes[t].pos)
+// and loc_to_pos(probes[t].agent, probes[t].seq) on the state reached so far (the README's two
+// mappings, cursor.rs:147-190 count_pos; answers as crdt_pos_to_loc / crdt_loc_to_pos).
+// Otherwise as crdt_apply_local.  The probed documents keep the order -> leaf map.
+typedef struct { uint32_t pos, agent, seq; } crdt_probe;
+typedef struct { uint32_t agent, seq, pos, deleted; } crdt_probe_answer;
+int crdt_apply_local_probed(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
+                            const crdt_local_txn* txns, const crdt_local_op* ops, const crdt_probe* probes,
+                            crdt_probe_answer* answers, int32_t* doc_status);
 int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23);
 /* Device time of the last replay / publish launches in ms (HIP events on the engine stream). */
 int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms);

@@ -125,6 +125,30 @@ int orc_apply_local_trace(void* h, uint16_t agent, uint32_t ntxn, const uint32_t
   return OK;
 }
 
+// Config 1's per-op check: after txn t, answer pos_to_loc(probes[3t]) and
+// loc_to_pos(probes[3t+1], probes[3t+2]) into answers[4t .. 4t+4) = (agent, seq, pos, deleted).
+// After a failing txn every later answer is 0xFFFFFFFF (the document stopped).
+void orc_pos_to_loc(void* h, uint32_t n, const uint32_t* pos, uint16_t* agent, uint32_t* seq);
+void orc_loc_to_pos(void* h, uint32_t n, const uint16_t* agent, const uint32_t* seq, uint32_t* pos, uint8_t* deleted);
+int orc_probe_trace(void* h, uint16_t agent, uint32_t ntxn, const uint32_t* counts, const uint32_t* patches3,
+                    const uint32_t* probes3, uint32_t* answers4) {
+  Doc* d = (Doc*)h;
+  const LocalOp* p = (const LocalOp*)patches3;
+  int st = OK;
+  for (uint32_t t = 0; t < ntxn; t++) {
+    uint32_t* a = answers4 + 4 * (size_t)t;
+    if (st == OK) st = d->apply_local_txn(agent, p, counts[t]);
+    p += counts[t];
+    if (st != OK) { a[0] = a[1] = a[2] = a[3] = 0xFFFFFFFFu; continue; }
+    uint16_t ag; uint32_t sq, ps; uint8_t dl;
+    orc_pos_to_loc(h, 1, probes3 + 3 * (size_t)t, &ag, &sq);
+    uint16_t qa = (uint16_t)probes3[3 * (size_t)t + 1];
+    orc_loc_to_pos(h, 1, &qa, probes3 + 3 * (size_t)t + 2, &ps, &dl);
+    a[0] = ag; a[1] = sq; a[2] = ps; a[3] = dl;
+  }
+  return st;
+}
+
 // n_ops generated local edits by `agent` (config 4), one LocalOp per txn.
 int orc_apply_random(void* h, uint16_t agent, uint32_t n_ops, uint32_t seed) {
   Doc* d = (Doc*)h;

@@ -1,6 +1,7 @@
-"""Diagnostic: per-path cycle attribution of k_replay (build with -DCRDT_PROF into
-build/libcrdt_gpu_prof.so, run with CRDT_GPU_LIB pointing at it).  Prints, per document averaged,
-the s_memtime cycles spent in fast paths vs the general interpreter."""
+"""Diagnostic: per-path attribution of k_replay (build with -DCRDT_PROF into
+build/libcrdt_gpu_prof.so, run with CRDT_GPU_LIB pointing at it).  Documents d % 4 == 0 record
+s_memtime cycles per path, d % 4 == 1 calls per path, d % 4 == 2 txns per path (config 2: every
+document replays the same trace, so the three views combine)."""
 import os
 import sys
 
@@ -8,17 +9,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "text-crdt-rust_amd"))
 import numpy as np  # noqa: E402
 import crdt_amd  # noqa: E402
-from crdt_amd.traces import load_remote_wire  # noqa: E402
+from crdt_amd.traces import load_remote_wire, load_trace  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+local = len(sys.argv) > 2 and sys.argv[2] == "local"
 e = crdt_amd.Engine(n, 32)
-e.stage_remote_replicated(load_remote_wire("automerge-paper"), 0, ["u%05d" % i for i in range(n)])
+if local:
+    t = load_trace("automerge-paper")
+    ag = e.agent_intern(list(range(n)), ["jeremy"] * n)
+    e.apply_trace(list(range(n)), int(ag[0]), t.counts, t.patches, stage_only=True)
+else:
+    e.stage_remote_replicated(load_remote_wire("automerge-paper"), 0, ["u%05d" % i for i in range(n)])
 e.run()
 e.reset_async()
 e.run_async()
 e.sync()
 ms = e.timings()[0]
-s = np.array([e.debug_state(d) for d in range(0, n, max(1, n // 64))]).astype(np.float64)
-c = {"typing": s[:, 18].mean(), "generic": s[:, 19].mean(), "delete": s[:, 20].mean(), "insert": s[:, 21].mean()}
-tot = sum(c.values())
-print(f"docs {n} replay_ms {ms:.1f}  per-doc clock ticks: " + "  ".join(f"{k} {v:.4g} ({v / tot:.1%})" for k, v in c.items()))
+P0 = 19  # DocState.prof0
+names = ["typing", "generic", "delete", "insert"]
+view = {}
+for m, lab in enumerate(["cycles", "calls", "txns"]):
+    s = np.array([e.debug_state(d) for d in range(m, n, 4 * max(1, n // 256))]).astype(np.float64)
+    view[lab] = s[:, P0:P0 + 4].mean(axis=0)
+tot = view["cycles"].sum()
+print(f"docs {n} {'local' if local else 'remote'} replay_ms {e.timings()[0]:.1f}")
+for i, k in enumerate(names):
+    c, calls, tx = view["cycles"][i], view["calls"][i], view["txns"][i]
+    print(f"  {k:8s} cycles {c:.4g} ({c / tot:.1%})  calls {calls:.0f}  txns {tx:.0f}  cycles/call {c / max(calls, 1):.0f}  cycles/txn {c / max(tx, 1):.0f}")
+s = np.array([e.debug_state(d) for d in range(3, n, 4 * max(1, n // 256))]).astype(np.float64)[:, P0:P0 + 4].mean(axis=0)
+print(f"  detail (cycles): split_at {s[0]:.4g}  apply_txn {s[1]:.4g} ({s[1] / tot:.1%})  failed fast attempts {s[2]:.4g} ({s[2] / tot:.1%})  fast ok {s[3]:.4g} ({s[3] / tot:.1%})")

@@ -28,6 +28,7 @@ struct EmuDoc {
   std::vector<AgentRec> agent_tab;
   std::vector<GroupRec> groups;
   std::vector<Rec> recs;
+  std::vector<uint4> probe;
   DocSeg seg{};
   DocState st{};
   bool inited = false;
@@ -50,6 +51,7 @@ struct EmuDoc {
     p.agents = agent_tab.data();
     p.groups = groups.data();
     p.recs = recs.data();
+    p.probe = probe.empty() ? nullptr : probe.data();
     p.seg = &seg;
     p.st = &st;
     return p;
@@ -183,8 +185,33 @@ int emu_run_local(void* h, uint16_t agent, uint32_t ntxn, const uint32_t* counts
   d->recs.clear();
   const uint32_t* p = patches3;
   for (uint32_t t = 0; t < ntxn; t++) { encode_local_txn(d->recs, nd, agent, p, counts[t]); p += 3 * counts[t]; }
-  d->prepare(nd, true, leaf_div);
+  d->prepare(nd, false, leaf_div);  // local streams never read the order -> leaf map (untracked)
   return d->run();
+}
+
+// local trace with a PROBE record after every txn; answers4 gets (agent, seq, pos, deleted)
+int emu_run_local_probed(void* h, uint16_t agent, uint32_t ntxn, const uint32_t* counts, const uint32_t* patches3,
+                         const uint32_t* probes3, uint32_t* answers4, uint32_t leaf_div) {
+  EmuDoc* d = (EmuDoc*)h;
+  StreamNeeds nd;
+  d->recs.clear();
+  std::vector<size_t> at;
+  const uint32_t* p = patches3;
+  for (uint32_t t = 0; t < ntxn; t++) {
+    encode_local_txn(d->recs, nd, agent, p, counts[t]);
+    p += 3 * counts[t];
+    at.push_back(d->recs.size());
+    encode_probe(d->recs, nd, probes3[3 * t], probes3[3 * t + 1], probes3[3 * t + 2]);
+  }
+  d->probe.assign(d->recs.size(), make_uint4(~0u, ~0u, ~0u, ~0u));
+  d->prepare(nd, true, leaf_div);
+  int st = d->run();
+  for (uint32_t t = 0; t < ntxn; t++) {
+    const uint4& x = d->probe[at[t]];
+    answers4[4 * t] = x.x; answers4[4 * t + 1] = x.y; answers4[4 * t + 2] = x.z; answers4[4 * t + 3] = x.w;
+  }
+  d->probe.clear();
+  return st;
 }
 
 int emu_run_random(void* h, uint16_t agent, uint32_t n_ops, uint32_t seed, uint32_t leaf_div) {
@@ -192,7 +219,7 @@ int emu_run_random(void* h, uint16_t agent, uint32_t n_ops, uint32_t seed, uint3
   StreamNeeds nd;
   d->recs.clear();
   encode_gen(d->recs, nd, agent, n_ops, seed);
-  d->prepare(nd, true, leaf_div);
+  d->prepare(nd, false, leaf_div);
   return d->run();
 }
 

@@ -256,6 +256,16 @@ struct WaveCPU {
     }
     return false;
   }
+  u32 root_vis_before(u32 g) const { u32 t = 0; for (u32 i = 0; i < g; i++) t += gv[i]; return t; }
+  u32 blk_vis_before(const u32* dv, u32 i) const { u32 t = 0; for (u32 k = 0; k < i; k++) t += dv[k]; return t; }
+  u32 cache_vis_before(u32 idx) const { u32 t = 0; for (u32 i = 0; i < idx; i++) t += clen(c[i]); return t; }
+  u32 peek_vis_before(const Span* p, u32 idx, i32& len_idx) const {
+    u32 t = 0;
+    for (u32 i = 0; i < idx; i++) t += clen(p[i]);
+    len_idx = p[idx].len;
+    return t;
+  }
+  void st_probe(uint4* p, u32 a, u32 s, u32 ps, u32 dl) const { *p = make_uint4(a, s, ps, dl); }
   bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
     u32 acc = 0;
     for (u32 k = 0; k < cnt; k++) {

@@ -34,6 +34,7 @@ def lib():
         L.emu_run_local.argtypes = [vp, u16, u32, P(u32), P(u32), u32]
         L.emu_run_wire.argtypes = [vp, C.c_char_p, C.c_size_t, u32]
         L.emu_run_random.argtypes = [vp, u16, u32, u32, u32]
+        L.emu_run_local_probed.argtypes = [vp, u16, u32, P(u32), P(u32), P(u32), P(u32), u32]
         L.emu_sizes.argtypes = [vp, P(C.c_uint64)]
         L.emu_export.argtypes = [vp] + [P(u32)] * 8
         L.emu_check.argtypes = [vp, C.c_char_p, C.c_int]
@@ -61,6 +62,14 @@ class EmuDoc:
         c = np.ascontiguousarray(counts, dtype=np.uint32)
         p = np.ascontiguousarray(patches, dtype=np.uint32)
         return self.L.emu_run_local(self.h, agent, c.shape[0], _p(c), _p(p), leaf_div)
+
+    def run_local_probed(self, agent, counts, patches, probes, leaf_div: int = 48):
+        c = np.ascontiguousarray(counts, dtype=np.uint32)
+        p = np.ascontiguousarray(patches, dtype=np.uint32)
+        q = np.ascontiguousarray(probes, dtype=np.uint32).reshape(-1, 3)
+        ans = np.zeros((c.shape[0], 4), np.uint32)
+        st = self.L.emu_run_local_probed(self.h, agent, c.shape[0], _p(c), _p(p), _p(q), _p(ans), leaf_div)
+        return st, ans
 
     def run_wire(self, wire: bytes, leaf_div: int = 48) -> int:
         return self.L.emu_run_wire(self.h, wire, len(wire), leaf_div)

@@ -202,3 +202,22 @@ def config5_wire(seed: int, base_len: int = 4096, n_agents: int = 16, rounds: in
             txns.append(per_agent[a].pop(0))
         frontier = [(a, seq[a] - 1) for a in names]
     return build_wire(txns)
+
+
+def config1_probes(counts, patches, agent: int, seed=None):
+    """BASELINE config 1's per-op check: after every txn, pos_to_loc(the txn's first op position)
+    and loc_to_pos(the txn's first item = (agent, seq of its first order)).  With `seed`, every
+    other probe instead asks a random position (up to 2 past the end) and a random earlier seq."""
+    c = np.asarray(counts, dtype=np.int64)
+    p = np.asarray(patches, dtype=np.int64).reshape(-1, 3)
+    first_op = np.concatenate([[0], np.cumsum(c)[:-1]])
+    op_len = p[:, 1] + p[:, 2]
+    txn_len = np.add.reduceat(op_len, first_op) if len(c) else np.zeros(0, np.int64)
+    seq0 = np.concatenate([[0], np.cumsum(txn_len)[:-1]])
+    pr = np.stack([p[first_op, 0], np.full(len(c), agent), seq0], 1)
+    if seed is not None:
+        rng = np.random.default_rng(seed)
+        k = np.arange(len(c)) % 2 == 1
+        pr[k, 0] = rng.integers(0, np.maximum(p[first_op[k], 0] + 3, 1))
+        pr[k, 2] = rng.integers(0, seq0[k] + txn_len[k])
+    return pr.astype(np.uint32)

@@ -55,6 +55,7 @@ def lib():
     L.orc_stats.argtypes = [vp, P(u64)]
     L.orc_text.argtypes = [vp, P(u32), u64, P(u32), u64, P(u64)]
     L.orc_text.restype = i64
+    L.orc_probe_trace.argtypes = [vp, u16, u32, P(u32), P(u32), P(u32), P(u32)]
     L.orc_dd_new.restype = vp
     L.orc_dd_free.argtypes = [vp]
     L.orc_dd_increment.argtypes = [vp, u32, u32]
@@ -108,6 +109,16 @@ class OracleDoc:
 
     def apply_remote_wire(self, wire: bytes) -> int:
         return self.L.orc_apply_remote_wire(self.h, wire, len(wire))
+
+    def probe_trace(self, agent: int, counts, patches, probes):
+        """apply the trace; after txn t answer pos_to_loc(probes[t,0]) and loc_to_pos(probes[t,1:3]);
+        returns (status, answers [T, 4])"""
+        c = np.ascontiguousarray(counts, dtype=np.uint32)
+        p = np.ascontiguousarray(patches, dtype=np.uint32)
+        q = np.ascontiguousarray(probes, dtype=np.uint32).reshape(-1, 3)
+        ans = np.zeros((c.shape[0], 4), np.uint32)
+        st = self.L.orc_probe_trace(self.h, agent, c.shape[0], _p(c), _p(p), _p(q), _p(ans))
+        return st, ans
 
     def apply_random(self, agent: int, n_ops: int, seed32: int) -> int:
         """config 4 generator (crdt_oracle.hpp random_change), n_ops local txns."""

@@ -110,3 +110,23 @@ def test_config5_full_size(L):
     assert e.check() == ""
     assert diff_states(o.export(), e.export()) == []
     assert e.sizes()["frontier"] == 16 and e.sizes()["grow_mask"] & 128
+
+
+@pytest.mark.parametrize("name", ["sveltecomponent", "automerge-paper"])
+@pytest.mark.parametrize("L", [32, 4])
+def test_config1_probes(name, L):
+    # BASELINE config 1: every txn of the trace followed by a pos->loc and a loc->pos query on the
+    # live state (PROBE records), answered by the replay core like the oracle's count_pos
+    from fuzz_gen import config1_probes
+    t = load_trace(name)
+    for seed in (None, 3):
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        a = o.agent("jeremy")
+        q = config1_probes(t.counts, t.patches, a, seed)
+        so, oans = o.probe_trace(a, t.counts, t.patches, q)
+        e = EmuDoc(L)
+        se, eans = e.run_local_probed(e.agent("jeremy"), t.counts, t.patches, q, 48 if L == 32 else 4)
+        assert so == se == 0
+        bad = np.argwhere((eans != oans).any(1))
+        assert bad.size == 0, (int(bad[0][0]), eans[bad[0][0]], oans[bad[0][0]])
+        assert (oans[:, 3] != 2).any() and (oans[:, 3] == 2).any()

@@ -143,3 +143,71 @@ def test_republish_after_different_history():
     for d in (0, 1):
         gp, gdl = e.loc_to_pos(np.full(seqs.shape[0], d, np.uint32), np.full(seqs.shape[0], ag[d], np.uint16), seqs)
         assert np.array_equal(gdl, odl) and np.array_equal(gp, op)
+
+
+def _wire_of_local(doc, agent, counts, patches):
+    """the remote wire of `agent`'s local txns applied to oracle `doc` (and applies them)."""
+    import ctypes as C
+    from oracle_lib import lib, _p
+    c = np.ascontiguousarray(counts, np.uint32)
+    p = np.ascontiguousarray(patches, np.uint32)
+    buf = C.create_string_buffer(64 << 20)
+    n = lib().orc_local_trace_to_wire(doc.h, agent, c.shape[0], _p(c), _p(p), C.cast(buf, C.c_void_p), 64 << 20)
+    assert n > 0
+    return buf.raw[:n]
+
+
+def test_local_document_starts_keeping_the_order_map():
+    # Documents that only apply local txns keep no order -> leaf map (remote ops alone read it).
+    # The first remote stream makes the engine rebuild it from the leaves: agent B's remote txns
+    # then resolve their origins (A's items) through it.
+    from crdt_amd.traces import load_trace
+    sv = load_trace("sveltecomponent")
+    cA, cB = sv.counts[:3000], sv.counts[3000:3600]
+    pA = sv.patches[: int(cA.sum())]
+    pB = sv.patches[int(cA.sum()): int(cA.sum()) + int(cB.sum())]
+    o = OracleDoc()
+    a = o.agent("A")
+    assert o.apply_trace(a, cA, pA) == 0
+    wB = _wire_of_local(o, o.agent("B"), cB, pB)
+    e = crdt_amd.Engine(2, 32)
+    ag = e.agent_intern([0, 1], ["A", "A"])
+    assert (e.apply_trace([0, 1], int(ag[0]), cA, pA) == 0).all()
+    st = e.apply_remote_wire([1], [wB])
+    assert st[0] == 0
+    assert_same(e.export(1), o.export())
+    assert int(e.digests()[1]) == o.digest()
+    check_queries(e, 1, o)
+    # doc 0 stayed local-only and still matches its own history
+    o0 = OracleDoc()
+    o0.apply_trace(o0.agent("A"), cA, pA)
+    assert int(e.digests()[0]) == o0.digest()
+
+
+def test_fit_then_replay():
+    # crdt_fit shrinks every capacity to the staged streams' use; a reset + replay of the same
+    # streams then runs in exactly that room (no growth) and publishes the same state
+    from crdt_amd.traces import load_trace, load_remote_wire
+    w = load_remote_wire("sveltecomponent")
+    t = load_trace("rustcode")
+    e = crdt_amd.Engine(2, 32)
+    assert e.apply_remote_wire([0], [w])[0] == 0
+    dg0 = e.digests()
+    b0 = e.mem_bytes()
+    e.fit()
+    assert e.mem_bytes() <= b0
+    e.reset_async()
+    e.run_async()
+    e.sync()
+    assert (e.status() == 0).all()
+    assert (e.digests() == dg0).all()
+    o = OracleDoc()
+    o.apply_remote_wire(w)
+    assert_same(e.export(0), o.export())
+    check_queries(e, 0, o)
+    # a new stream after a fit grows the capacities back
+    ag = e.agent_intern([1], ["jeremy"])
+    assert e.apply_trace([1], int(ag[0]), t.counts, t.patches)[0] == 0
+    o2 = OracleDoc()
+    o2.apply_trace(o2.agent("jeremy"), t.counts, t.patches)
+    assert int(e.digests()[1]) == o2.digest()

@@ -296,3 +296,35 @@ def test_config5_full_size():
                 assert_same(e.export(i), o.export())
             if i == 0:
                 check_queries_sampled(e, 0, o)
+
+
+@pytest.mark.parametrize("L", [32, 4])
+def test_config1_every_op_probed(L):
+    # BASELINE config 1 ("checking every position <-> CRDT-location lookup"): after EVERY txn of
+    # automerge-paper (and rustcode), pos_to_loc(the op's position) and loc_to_pos(the txn's first
+    # item) on the live state, in the replay kernel (PROBE records), against the oracle after the
+    # same txn; a second pass probes random positions / earlier items instead
+    from fuzz_gen import config1_probes
+    names = ["automerge-paper", "rustcode"]
+    traces = [load_trace(n) for n in names]
+    for seed in (None, 11):
+        e = crdt_amd.Engine(len(traces), L)
+        ag = e.agent_intern(list(range(len(traces))), ["jeremy"] * len(traces))
+        tx, ops, pr, off = [], [], [], [0]
+        oans = []
+        for d, t in enumerate(traces):
+            tx.append(np.stack([np.full(len(t.counts), ag[d]), t.counts], 1))
+            ops.append(t.patches)
+            q = config1_probes(t.counts, t.patches, int(ag[d]), seed)
+            pr.append(q)
+            off.append(off[-1] + len(t.counts))
+            o = OracleDoc(L, 16 if L == 32 else 8)
+            so, a = o.probe_trace(o.agent("jeremy"), t.counts, t.patches, q)
+            assert so == 0
+            oans.append(a)
+        st, ans = e.apply_local_probed(list(range(len(traces))), off, np.concatenate(tx), np.concatenate(ops),
+                                       np.concatenate(pr))
+        assert (st == 0).all(), st
+        oans = np.concatenate(oans)
+        bad = np.argwhere((ans != oans).any(1))
+        assert bad.size == 0, (int(bad[0][0]), ans[bad[0][0]], oans[bad[0][0]])

@@ -84,6 +84,10 @@ def lib():
     L.crdt_stage_random.argtypes = [vp, u64, P(u32), C.c_char_p, u32, u64]
     L.crdt_stage_local_shared.argtypes = [vp, u64, P(u32), P(u32), u32, P(u64), vp, vp]
     L.crdt_debug_state.argtypes = [vp, u32, P(u32)]
+    L.crdt_fit.argtypes = [vp]
+    L.crdt_apply_local_probed.argtypes = [vp, u64, P(u32), P(u64), vp, vp, vp, vp, P(i32)]
+    L.crdt_mem_bytes.argtypes = [vp]
+    L.crdt_mem_bytes.restype = u64
     L.crdt_reset_async.argtypes = [vp]
     L.crdt_run.argtypes = [vp, P(i32)]
     L.crdt_run_async.argtypes = [vp]
@@ -126,7 +130,7 @@ EXPORTED_SYMBOLS = [
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
-    "crdt_last_materialize_ms", "crdt_set_content_copies",
+    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed",
     # include/crdt_trace.h (host-only trace ingestion)
     "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
@@ -191,6 +195,21 @@ class Engine:
 
     def apply_local(self, per_doc) -> np.ndarray:
         return self.apply_local_arrays(*self._local_arrays(per_doc))
+
+    def apply_local_probed(self, d, off, tx, ops, probes):
+        """apply_local_arrays with one probe (pos, agent, seq) after every txn; returns (status,
+        answers [T, 4] = (agent, seq) of pos, (pos, deleted) of (agent, seq))"""
+        d = np.ascontiguousarray(d, dtype=np.uint32)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        tx = np.ascontiguousarray(tx, dtype=np.uint32).reshape(-1, 2)
+        ops = np.ascontiguousarray(ops, dtype=np.uint32).reshape(-1, 3)
+        pr = np.ascontiguousarray(probes, dtype=np.uint32).reshape(-1, 3)
+        ans = np.zeros((tx.shape[0], 4), np.uint32)
+        st = np.zeros(d.shape[0], np.int32)
+        _check(self.L.crdt_apply_local_probed(self.h, d.shape[0], _p(d), _p(off, C.c_uint64), tx.ctypes.data,
+                                              ops.ctypes.data, pr.ctypes.data, ans.ctypes.data, _p(st, C.c_int32)),
+               "apply_local_probed")
+        return st, ans
 
     def apply_local_arrays(self, d, off, tx, ops) -> np.ndarray:
         """crdt_apply_local on CSR arrays: docs [n], txn_off [n+1] (u64), txns [T,2] (agent, n_ops),
@@ -268,6 +287,14 @@ class Engine:
         out = np.zeros(23, np.uint32)
         _check(self.L.crdt_debug_state(self.h, doc, _p(out)), "debug_state")
         return out
+
+    def fit(self):
+        """shrink capacities to the staged streams' use (after run + publish)"""
+        _check(self.L.crdt_fit(self.h), "fit")
+
+    def mem_bytes(self) -> int:
+        """device bytes held by the per-document pools + staged records"""
+        return int(self.L.crdt_mem_bytes(self.h))
 
     def reset_async(self):
         _check(self.L.crdt_reset_async(self.h), "reset")

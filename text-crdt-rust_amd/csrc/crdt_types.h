@@ -97,7 +97,7 @@ struct GroupRec { u32 blk, cnt, vis, pad; };   // persisted root level of the di
 // Op record stream (16 B records, per document, in causal order)
 // ---------------------------------------------------------------------------------------------
 enum : u32 { REC_LTXN = 1, REC_LOP = 2, REC_RTXN = 3, REC_RINS = 4, REC_RDEL = 5, REC_RPARENT = 6, REC_GEN = 7,
-             REC_RC = 8, REC_LC = 9 };
+             REC_RC = 8, REC_LC = 9, REC_PROBE = 10 };
 struct Rec { u32 w0, w1, w2, w3; };
 // LTXN    w0 = kind<<28 | n_ops         w1 = agent                  w2 = sum(del) w3 = txn_len
 // LOP     w0 = kind<<28                 w1 = pos                    w2 = del   w3 = ins
@@ -116,6 +116,9 @@ struct Rec { u32 w0, w1, w2, w3; };
 //         one RemoteOp; its origins / target are the author's items (a seq of 0xFFFFFFFF names
 //         ROOT); the one parent is (author, seq - 1)
 // LC      w0 = kind<<28 | agent (16 b)  w1 = pos   w2 = del   w3 = ins   (one LocalOp)
+// PROBE   w0 = kind<<28                 w1 = pos   w2 = agent w3 = seq
+//         answers pos -> (agent, seq) and (agent, seq) -> (pos, deleted) on the state reached so far
+//         (config 1's per-op check); the answer goes to probe_out[record index]
 CRDT_HD u32 rec_kind(const Rec& r) { return r.w0 >> 28; }
 constexpr u32 RC_HDR_MASK = 0xF800FFFFu;  // kind | del | author (not len)
 CRDT_HD u32 rc_len(const Rec& r) { return (r.w0 >> 16) & 0x7FFu; }
@@ -162,6 +165,8 @@ CRDT_HD Rec gen_op(u32 seed, u32 i, u32 len) {
 // ---------------------------------------------------------------------------------------------
 // Per-document segments (host-assigned, read-only during replay) and mutable header
 // ---------------------------------------------------------------------------------------------
+// DOC_TRACK_MAP: the document keeps its order -> leaf map (the SplitList replacement), which only
+// remote ops read (find_order); documents that only ever apply local ops skip it entirely.
 enum : u32 { DOC_TRACK_MAP = 1u };
 
 struct DocSeg {
@@ -175,7 +180,13 @@ struct DocSeg {
   u32 arun_cap, del_cap, dd_cap, txn_cap;
   u32 par_cap, agent_cap, rec_n, flags;
   u32 fr_cap, grp_cap;  // frontier heads; root groups (= blk_cap)
+  // published index (k_publish): canonical spans + vpos + rank -> span at canon_base (canon_cap
+  // spans); the span-start bitmap and its per-word prefix at pub_base (2 x pub_words(ord_cap)
+  // words); text (k_materialize) at ord_base (ord_cap code points); ord_cap > every order
+  u64 canon_base, pub_base, ord_base;
+  u32 canon_cap, ord_cap;
 };
+CRDT_HD u32 pub_words(u32 ord_cap) { return ord_cap / 32u + 1u; }
 
 struct DocState {
   i32 status;
@@ -200,6 +211,7 @@ struct Pools {
   DelRun* dels;
   DDRun* dd;
   DDBlk* ddb;
+  uint4* probe;        // [rec_base + record]: answers of PROBE records (nullptr: none staged)
   TxnRec* txns;
   u32* parents;
   u32* frontier;       // [fr_base .. + fr_cap]

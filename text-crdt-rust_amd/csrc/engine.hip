@@ -61,12 +61,13 @@ struct PoolSet {
   AgentRec* agents = nullptr;
   Span* canon = nullptr;
   u32* vpos = nullptr;
-  u32* span_of = nullptr;
+  u32* sorted = nullptr;
+  u32* pub = nullptr;
   u64 bytes = 0;
   void free_all() {
     dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(cwo); dfree(arun);
     dfree(dels); dfree(dd); dfree(ddb); dfree(txns); dfree(parents); dfree(frontier); dfree(groups); dfree(agents); dfree(canon);
-    dfree(vpos); dfree(span_of);
+    dfree(vpos); dfree(sorted); dfree(pub);
     bytes = 0;
   }
 };
@@ -75,7 +76,8 @@ struct DocHost {
   AgentTable agents;
   StreamNeeds cum;          // needs of every stream applied since the last reset (capacity plan)
   StreamNeeds staged;       // needs of the stream staged now (a reset replays it: cum = staged)
-  Caps caps{};              // current capacities (never shrink)
+  Caps caps{};              // current capacities (grow; crdt_fit shrinks them to the replay's use)
+  bool tracked = false;     // keeps the order -> leaf map (once a remote stream was staged)
   std::vector<u32> agent_cap;
 };
 
@@ -84,6 +86,8 @@ inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
   c.local_del += n.local_del; c.remote_del_ops += n.remote_del_ops; c.remote_parents += n.remote_parents;
   if (c.txns_per_agent.size() < n.txns_per_agent.size()) c.txns_per_agent.resize(n.txns_per_agent.size(), 0);
   for (size_t a = 0; a < n.txns_per_agent.size(); a++) c.txns_per_agent[a] += n.txns_per_agent[a];
+  c.txn_max(n.max_ops, n.max_del, n.max_len, n.max_parents);
+  c.probes += n.probes;
 }
 
 // Launch shape of a wave-per-document kernel whose waves hold an LDS root of `rcap` groups:
@@ -127,6 +131,9 @@ struct crdt_engine {
   PoolSet pools;
   Rec* recs = nullptr;
   u64 rec_cap = 0;
+  uint4* probe = nullptr;  // PROBE answers, one slot per staged record (when probes are staged)
+  u64 probe_cap = 0;
+  bool has_probes = false;
   bool published = false;
   double last_replay_ms = 0, last_publish_ms = 0, last_materialize_ms = 0;
   // text materialisation: order-indexed content streams, per-document stream offsets, output text
@@ -137,7 +144,7 @@ struct crdt_engine {
   u64* clen = nullptr;
   u32* text = nullptr;
   u64 text_cap = 0;
-  u64 map_total = 0;
+  u64 ord_total = 0;  // text buffer entries (sum of ord_cap)
   u32* tlen = nullptr;
   u64* tdigest = nullptr;
   bool materialized = false;
@@ -163,6 +170,7 @@ struct crdt_engine {
     p.agents = ps.agents;
     p.groups = ps.groups;
     p.recs = recs;
+    p.probe = has_probes ? probe : nullptr;
     p.seg = segs;
     p.st = st;
     return p;
@@ -171,7 +179,8 @@ struct crdt_engine {
     PubOut o{};
     o.canon = pools.canon;
     o.vpos = pools.vpos;
-    o.span_of = pools.span_of;
+    o.sorted = pools.sorted;
+    o.pub = pools.pub;
     o.canon_n = canon_n;
     o.len = len;
     o.digest = digest;
@@ -185,6 +194,9 @@ struct crdt_engine {
     classes.clear();
     dfree(recs);
     rec_cap = 0;
+    dfree(probe);
+    probe_cap = 0;
+    has_probes = false;
     dfree(content); dfree(cbase); dfree(clen); dfree(text); dfree(tlen); dfree(tdigest);
     content_cap = 0;
     text_cap = 0;
@@ -236,6 +248,7 @@ struct crdt_engine {
     int r = 0;
     PoolSet np;
     u64 nl = 0, nb = 0, nm = 0, nc = 0, na = 0, ndl = 0, ndd = 0, nt = 0, npar = 0, nag = 0, nfr = 0;
+    u64 ncan = 0, npub = 0, nord = 0;
     std::vector<DocSeg> nseg(n_docs);
     std::vector<AgentRec> agent_tab;
     std::vector<u32> n_agents(n_docs);
@@ -252,6 +265,11 @@ struct crdt_engine {
       s.txn_base = nt; s.txn_cap = c.txn; nt += c.txn;
       s.par_base = npar; s.par_cap = c.par; npar += c.par;
       s.fr_base = nfr; s.fr_cap = c.fr; nfr += c.fr;
+      s.canon_cap = c.canon ? c.canon : (u32)std::min<u64>((u64)c.leaf * L, 0xFFFFFFFFull);
+      s.canon_base = ncan; ncan += s.canon_cap;
+      s.ord_cap = std::max<u32>(c.ord, 1u);
+      s.ord_base = nord; nord += s.ord_cap;
+      s.pub_base = npub; npub += 2ull * pub_words(s.ord_cap);
       s.grp_base = s.blk_base; s.grp_cap = c.blk;  // one root group per directory block
       s.agent_base = nag;
       u32 ag = (u32)h.agents.names.size();
@@ -271,7 +289,7 @@ struct crdt_engine {
       s.arun_cap = rb;
       na += rb;
       nag += ag;
-      s.flags = DOC_TRACK_MAP;
+      s.flags = h.tracked ? DOC_TRACK_MAP : 0u;
       s.rec_base = seg_h[d].rec_base;
       s.rec_n = seg_h[d].rec_n;
       nseg[d] = s;
@@ -281,7 +299,6 @@ struct crdt_engine {
     HIPCHK(dalloc(np.dir_leaf, nb * GROUP));
     HIPCHK(dalloc(np.dir_vis, nb * GROUP));
     HIPCHK(dalloc(np.leaf_of, nm));
-    HIPCHK(dalloc(np.span_of, nm));
     HIPCHK(dalloc(np.cwo, nc));
     HIPCHK(dalloc(np.arun, na));
     HIPCHK(dalloc(np.dels, ndl));
@@ -292,10 +309,12 @@ struct crdt_engine {
     HIPCHK(dalloc(np.frontier, nfr));
     HIPCHK(dalloc(np.groups, nb));
     HIPCHK(dalloc(np.agents, nag));
-    HIPCHK(dalloc(np.canon, nl * L));
-    HIPCHK(dalloc(np.vpos, nl * L));
-    np.bytes = nl * L * (16 + 16 + 4) + nl * 4 + nb * GROUP * 8 + nm * 8 + nc * 16 + na * 16 + ndl * 12 + ndd * (DD_BLK * 12 + 16) +
-               nt * 32 + npar * 4 + nag * 16 + nfr * 4 + nb * 16;
+    HIPCHK(dalloc(np.canon, ncan));
+    HIPCHK(dalloc(np.vpos, ncan));
+    HIPCHK(dalloc(np.sorted, ncan));
+    HIPCHK(dalloc(np.pub, npub));
+    np.bytes = nl * L * 16 + ncan * 24 + npub * 4 + nl * 4 + nb * GROUP * 8 + nm * 4 + nc * 16 + na * 16 + ndl * 12 +
+               ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * 16 + nfr * 4 + nb * 16;
     if (!agent_tab.empty())
       HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(n_agents_d, n_agents.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
@@ -320,7 +339,7 @@ struct crdt_engine {
     seg_h = nseg;
     r = plan_classes();
     if (r) return r;
-    map_total = nm;
+    ord_total = nord;
     published = false;
     materialized = false;
     return 0;
@@ -415,16 +434,34 @@ struct crdt_engine {
       for (u64 d = 0; d < n_docs; d++)
         if (!seen[d]) docs[d].staged = StreamNeeds{};
     }
-    // cumulative needs -> capacities
+    // documents that receive their first remote stream start keeping the order -> leaf map (only
+    // remote ops read it); one that already holds state gets it rebuilt from its leaves
+    std::vector<u32> rebuild;
+    bool pulled = false;
     bool grow = false;
+    for (size_t i = 0; i < doc_ids.size(); i++) {
+      DocHost& h = docs[doc_ids[i]];
+      if (h.tracked || (needs[i].n_rtxn == 0 && needs[i].probes == 0)) continue;
+      h.tracked = true;
+      grow = true;
+      if (!pulled) {
+        r = pull_states();
+        if (r) return r;
+        pulled = true;
+      }
+      if (st_h[doc_ids[i]].next_order) rebuild.push_back((u32)doc_ids[i]);
+    }
+    // cumulative needs -> capacities
     for (size_t i = 0; i < doc_ids.size(); i++) {
       DocHost& h = docs[doc_ids[i]];
       StreamNeeds& c = h.cum;
       add_needs(c, needs[i]);
       h.staged = needs[i];
-      Caps nc = plan_caps(c, (u32)h.agents.names.size(), true, 48);
+      Caps nc = plan_caps(c, (u32)h.agents.names.size(), h.tracked, 48);
       Caps& oc = h.caps;
       auto up = [&](u32& o, u32 v) { if (v > o) { o = v; grow = true; } };
+      up(oc.ord, nc.ord);
+      if (oc.canon) { oc.canon = 0; grow = true; }  // a fitted canonical-span capacity: back to the bound
       up(oc.leaf, nc.leaf); up(oc.blk, nc.blk); up(oc.map, nc.map); up(oc.cwo, nc.cwo); up(oc.arun, nc.arun);
       up(oc.del, nc.del); up(oc.dd, nc.dd); up(oc.txn, nc.txn); up(oc.par, nc.par); up(oc.agent, nc.agent);
       up(oc.fr, nc.fr);
@@ -436,12 +473,19 @@ struct crdt_engine {
       if (h.agents.names.size() != h.agent_cap.size()) grow = true;
     }
     // records: one buffer for this call
-    u64 total = 0;
+    u64 total = 0, n_probes = 0;
     for (auto* s : streams) total += s->size();
+    for (auto& n : needs) n_probes += n.probes;
     if (total > rec_cap) {
       dfree(recs);
       rec_cap = std::max<u64>(total, 1024);
       HIPCHK(dalloc(recs, rec_cap));
+    }
+    has_probes = n_probes > 0;
+    if (has_probes && probe_cap < total) {
+      dfree(probe);
+      probe_cap = total;
+      HIPCHK(dalloc(probe, probe_cap));
     }
     for (auto& sg : seg_h) { sg.rec_base = 0; sg.rec_n = 0; }
     // Consecutive distinct streams go up in one host->device copy; a replicated stream (same
@@ -492,6 +536,16 @@ struct crdt_engine {
     if (grow) {
       r = layout(true);
       if (r) return r;
+      if (!rebuild.empty()) {
+        u32* dl = nullptr;
+        HIPCHK(dalloc(dl, rebuild.size()));
+        HIPCHK(hipMemcpyAsync(dl, rebuild.data(), rebuild.size() * 4, hipMemcpyHostToDevice, stream));
+        if (L == 32) hipLaunchKernelGGL(k_build_map<32>, dim3((u32)rebuild.size()), dim3(256), 0, stream, pools_view(pools), (const u32*)dl, (u32)rebuild.size());
+        else hipLaunchKernelGGL(k_build_map<4>, dim3((u32)rebuild.size()), dim3(256), 0, stream, pools_view(pools), (const u32*)dl, (u32)rebuild.size());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(stream));
+        dfree(dl);
+      }
     } else {
       HIPCHK(hipMemcpyAsync(segs, seg_h.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
       r = push_agent_counts();
@@ -571,9 +625,51 @@ struct crdt_engine {
       r = layout(true);
       if (r) return r;
     }
+    // the published index and the text need room for every order (the estimate can be short for
+    // generated streams, and documents without the order map never stop for it)
+    bool grow_ord = false;
+    for (u64 d = 0; d < n_docs; d++)
+      if (st_h[d].next_order >= seg_h[d].ord_cap) {
+        docs[d].caps.ord = st_h[d].next_order + 1;
+        grow_ord = true;
+      }
+    if (grow_ord) {
+      r = layout(true);
+      if (r) return r;
+    }
     if (status_out)
       for (u64 d = 0; d < n_docs; d++) status_out[d] = st_h[d].status == ST_NEED_CAPACITY ? ST_CAPACITY : st_h[d].status;
     return 0;
+  }
+
+  // Shrink every document's capacities to what its staged stream used, keeping the room the
+  // replay reserves ahead of one txn (fits()): called after a full replay + publish of the staged
+  // streams, so that replaying them again (reset + run) needs exactly this much.
+  int fit() {
+    int r = ensure_published();
+    if (r) return r;
+    r = pull_states();
+    if (r) return r;
+    std::vector<u32> cn(n_docs);
+    HIPCHK(hipMemcpy(cn.data(), canon_n, n_docs * 4, hipMemcpyDeviceToHost));
+    for (u64 d = 0; d < n_docs; d++) {
+      const DocState& s = st_h[d];
+      if (s.status != ST_OK) continue;
+      DocHost& h = docs[d];
+      const StreamNeeds& m = h.cum;
+      Caps& c = h.caps;
+      c.leaf = std::max<u32>(s.n_leaves + 2 * m.max_ops + 2, 2);
+      c.blk = blk_cap_for(c.leaf);
+      c.cwo = s.n_cwo + 1;
+      c.txn = s.n_txn + 1;
+      c.del = s.n_del + m.max_del + 1;
+      c.par = s.n_par + std::max<u32>(m.max_parents, s.n_fr) + 64;
+      if (h.tracked) c.map = (u32)std::min<u64>((u64)s.next_order + m.max_len + 1, 0xFFFFFFFFull);
+      c.ord = s.next_order + 1;
+      c.canon = std::max<u32>(cn[d], 1);
+      c.fr = std::max<u32>(s.n_fr + 1, FRONTIER_CAP0);
+    }
+    return layout(true);
   }
 
   int publish() {
@@ -687,11 +783,11 @@ struct crdt_engine {
       r = publish();
       if (r) return r;
     }
-    if (text_cap < map_total) {
+    if (text_cap < ord_total) {
       HIPCHK(hipStreamSynchronize(stream));
       dfree(text);
-      HIPCHK(dalloc(text, map_total));
-      text_cap = std::max<u64>(map_total, 1);
+      HIPCHK(dalloc(text, ord_total));
+      text_cap = std::max<u64>(ord_total, 1);
     }
     HIPCHK(hipEventRecord(ev[4], stream));
     if (L == 32) hipLaunchKernelGGL(k_materialize<32>, dim3((u32)n_docs), dim3(64 * MAT_WAVES), 0, stream, pools_view(pools), pub_view(), text_view(), (u32)n_docs);
@@ -774,9 +870,12 @@ int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const cha
   return 0;
 }
 
+// probes (optional): one per txn, encoded after it; probe_rec gets each probe's record index
 static int stage_local_impl(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
-                            const crdt_local_txn* txns, const crdt_local_op* ops) {
+                            const crdt_local_txn* txns, const crdt_local_op* ops,
+                            const crdt_probe* probes = nullptr, std::vector<std::vector<u32>>* probe_rec = nullptr) {
   if (!valid(e) || !docs || !txn_off || (!txns && txn_off[n_docs]) ) return CRDT_E_ARG;
+  if (probe_rec) probe_rec->assign(n_docs, {});
   std::vector<u64> ids(n_docs);
   std::vector<std::vector<Rec>> streams(n_docs);
   std::vector<StreamNeeds> needs(n_docs);
@@ -791,9 +890,36 @@ static int stage_local_impl(crdt_engine* e, uint64_t n_docs, const uint32_t* doc
     for (u64 t = txn_off[i]; t < txn_off[i + 1]; t++) {
       encode_local_txn(streams[i], needs[i], txns[t].agent, (const u32*)(ops + op), txns[t].n_ops);
       op += txns[t].n_ops;
+      if (probes) {
+        (*probe_rec)[i].push_back((u32)streams[i].size());
+        encode_probe(streams[i], needs[i], probes[t].pos, probes[t].agent, probes[t].seq);
+      }
     }
   }
   return e->stage(ids, sp, needs);
+}
+
+int crdt_apply_local_probed(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
+                            const crdt_local_txn* txns, const crdt_local_op* ops, const crdt_probe* probes,
+                            crdt_probe_answer* answers, int32_t* doc_status) {
+  if (!probes || !answers) return CRDT_E_ARG;
+  std::vector<std::vector<u32>> where;
+  int r = stage_local_impl(e, n_docs, docs, txn_off, txns, ops, probes, &where);
+  if (r) return r;
+  std::vector<int32_t> all(e->n_docs);
+  r = e->run(all.data());
+  if (r) return r;
+  std::vector<uint4> buf(e->probe_cap);
+  HIPCHK(hipMemcpy(buf.data(), e->probe, buf.size() * sizeof(uint4), hipMemcpyDeviceToHost));
+  for (uint64_t i = 0; i < n_docs; i++) {
+    if (doc_status) doc_status[i] = all[docs[i]];
+    u64 base = e->seg_h[docs[i]].rec_base;
+    for (u64 t = txn_off[i], k = 0; t < txn_off[i + 1]; t++, k++) {
+      const uint4& x = buf[base + where[i][k]];
+      answers[t] = crdt_probe_answer{x.x, x.y, x.z, x.w};
+    }
+  }
+  return 0;
 }
 
 int crdt_stage_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
@@ -970,6 +1096,13 @@ int crdt_apply_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs
   return 0;
 }
 
+int crdt_fit(crdt_engine* e) {
+  if (!valid(e)) return CRDT_E_ARG;
+  int r = e->set_device();
+  if (r) return r;
+  return e->fit();
+}
+
 int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint32_t* pos, uint16_t* agent, uint32_t* seq) {
   if (!valid(e)) return CRDT_E_ARG;
   if (!e->published) {
@@ -1120,7 +1253,7 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
         li++;
       }
   }
-  if (canon4 && s[2]) HIPCHK(hipMemcpy(canon4, e->pools.canon + sg.leaf_base * L, s[2] * 16, hipMemcpyDeviceToHost));
+  if (canon4 && s[2]) HIPCHK(hipMemcpy(canon4, e->pools.canon + sg.canon_base, s[2] * 16, hipMemcpyDeviceToHost));
   if (cwo4 && st.n_cwo) HIPCHK(hipMemcpy(cwo4, e->pools.cwo + sg.cwo_base, st.n_cwo * 16, hipMemcpyDeviceToHost));
   if (del3 && st.n_del) HIPCHK(hipMemcpy(del3, e->pools.dels + sg.del_base, st.n_del * 12, hipMemcpyDeviceToHost));
   if (dd3 && st.n_dd) {  // flatten the blocks in directory order
@@ -1152,6 +1285,12 @@ int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23) {
   HIPCHK(hipMemcpyAsync(out23, e->st + doc, sizeof(DocState), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return 0;
+}
+
+uint64_t crdt_mem_bytes(const crdt_engine* e) {
+  if (!e) return 0;
+  return e->pools.bytes + e->rec_cap * sizeof(Rec) + e->content_cap * 4 + e->text_cap * 4 +
+         e->n_docs * (sizeof(DocState) + sizeof(DocSeg) + 4 + 4 + 8);
 }
 
 int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms) {
@@ -1191,7 +1330,7 @@ int crdt_text(crdt_engine* e, uint32_t doc, uint32_t* out, uint64_t cap, uint64_
   *n_out = n;
   if (!out) return 0;
   if (cap < n) return CRDT_E_ARG;
-  if (n) HIPCHK(hipMemcpy(out, e->text + e->seg_h[doc].map_base, (u64)n * 4, hipMemcpyDeviceToHost));
+  if (n) HIPCHK(hipMemcpy(out, e->text + e->seg_h[doc].ord_base, (u64)n * 4, hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -96,7 +96,16 @@ struct AgentTable {
 // Statistics of a record stream, for capacity planning.
 struct StreamNeeds {
   u64 n_txn = 0, n_ltxn = 0, n_rtxn = 0, n_ops = 0, orders = 0, local_del = 0, remote_del_ops = 0, remote_parents = 0;
+  // largest single txn (the replay checks room for one txn before applying it)
+  u32 max_ops = 0, max_del = 0, max_len = 0, max_parents = 0;
+  u64 probes = 0;  // PROBE records (their documents keep the order -> leaf map)
   std::vector<u32> txns_per_agent;
+  void txn_max(u32 ops, u64 del, u64 len, u32 parents) {
+    max_ops = std::max(max_ops, ops);
+    max_del = (u32)std::min<u64>(std::max<u64>(max_del, del), 0xFFFFFFFFull);
+    max_len = (u32)std::min<u64>(std::max<u64>(max_len, len), 0xFFFFFFFFull);
+    max_parents = std::max(max_parents, parents);
+  }
   void agent_txn(u32 a) {
     if (a >= 0xFFFE) return;
     if (txns_per_agent.size() <= a) txns_per_agent.resize(a + 1, 0);
@@ -110,6 +119,7 @@ inline void encode_local_txn(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, 
   for (u32 k = 0; k < nops; k++) { span += (u64)ops3[3 * k + 1] + ops3[3 * k + 2]; dels += ops3[3 * k + 1]; }
   u32 span32 = span > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)span;
   u32 dels32 = dels > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)dels;
+  nd.txn_max(nops, dels, span, 0);
   if (nops == 1 && agent <= 0xFFFFu && span <= 0xFFFFFFFFull) {  // one LocalOp: one compact record
     out.push_back(Rec{(REC_LC << 28) | agent, ops3[0], ops3[1], ops3[2]});
     nd.local_del += ops3[1];
@@ -148,6 +158,7 @@ inline void encode_remote(std::vector<Rec>& out, StreamNeeds& nd, AgentTable& at
       tl += len;
     }
     u32 tl32 = tl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)tl;
+    nd.txn_max(t.n_ops, t.n_ops, tl, t.n_parents);
     // the common shape -- one op on the author's own items (or ROOT), the author's previous txn
     // as the only parent -- is one compact record (crdt_types.h RC)
     if (t.n_ops == 1 && t.n_parents == 1 && author < 0xFFFEu && t.seq >= 1 && res(t.parents[0]) == author &&
@@ -199,11 +210,18 @@ inline void encode_remote(std::vector<Rec>& out, StreamNeeds& nd, AgentTable& at
   }
 }
 
+// A PROBE record: after the txns before it, answer pos_to_loc(pos) and loc_to_pos(agent, seq).
+inline void encode_probe(std::vector<Rec>& out, StreamNeeds& nd, u32 pos, u32 agent, u32 seq) {
+  out.push_back(Rec{REC_PROBE << 28, pos, agent, seq});
+  nd.probes++;
+}
+
 // One GEN record: `n_ops` local txns of one generated LocalOp each (gen_op, on the device).
 // Orders and delete runs are estimates (about 2.8 orders per op for make_random_change's
 // distribution); a table that fills stops the document resumably and grows.
 inline void encode_gen(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, u32 n_ops, u32 seed) {
   out.push_back(Rec{REC_GEN << 28, agent, n_ops, seed});
+  nd.txn_max(1, 10, 10, 0);  // make_random_change deletes <= 10 chars
   nd.n_txn += n_ops;
   nd.n_ltxn += n_ops;
   nd.n_ops += n_ops;
@@ -222,6 +240,8 @@ constexpr u32 MAX_LEAVES = 32 * (ROOT_CAP_MAX - 2);
 
 struct Caps {
   u32 leaf, blk, map, cwo, arun, del, dd, txn, par, agent, fr;
+  u32 ord;        // > every order the document will hold (published index, text)
+  u32 canon = 0;  // canonical spans (0: bounded by the leaf capacity, leaf * L)
 };
 inline u32 blk_cap_for(u32 leaf_cap) { return leaf_cap / 32 + 2; }
 // LDS root groups per wave for a document with `blk_cap` directory blocks (a multiple of 64)
@@ -238,6 +258,7 @@ inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_
   c.blk = blk_cap_for(c.leaf);
   c.fr = FRONTIER_CAP0;
   c.map = track ? (u32)std::min<u64>(nd.orders + 1, 0xFFFFFFFFull) : 0;
+  c.ord = (u32)std::min<u64>(nd.orders + 1, 0xFFFFFFFFull);
   // RLE tables usually coalesce far below one run per txn; start small and grow on demand
   // (ST_NEED_CAPACITY is resumable), exact bounds otherwise.
   c.cwo = (u32)std::min<u64>(nd.n_txn + 1, 256 + nd.n_txn / 64);

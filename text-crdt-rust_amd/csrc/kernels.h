@@ -13,13 +13,32 @@
 namespace crdt {
 
 struct PubOut {
-  Span* canon;    // [leaf_base*L + k]
-  u32* vpos;      // [leaf_base*L + k]  visible items before canonical span k
-  u32* span_of;   // [map_base + order]  canonical span containing item `order` (stale at delete orders)
+  Span* canon;    // [canon_base + k]
+  u32* vpos;      // [canon_base + k]  visible items before canonical span k
+  u32* sorted;    // [canon_base + r]  the canonical spans by first order (rank -> span)
+  u32* pub;       // [pub_base + w]    bit (o & 31) of word o >> 5: a canonical span starts at order o;
+                  // [pub_base + pub_words + w]  set bits in words [0, w)
   u32* canon_n;   // [doc]
   u32* len;       // [doc]
   u64* digest;    // [doc]
 };
+
+// Order -> canonical span through the published index: r = span starts at or below `order`;
+// the span is sorted[r - 1] if it contains the order (delete orders lie in no span).  Returns
+// the span index or INVALID.
+__device__ __forceinline__ u32 ld_l2(const u32* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ u32 span_of_order(const PubOut& O, const DocSeg& seg, u32 cn, u32 order) {
+  u32 nw = pub_words(seg.ord_cap);
+  const u32* bits = O.pub + seg.pub_base;
+  u32 wd = order >> 5;
+  if (wd >= nw) return INVALID;
+  u32 r = bits[nw + wd] + (u32)__popc(bits[wd] & (0xFFFFFFFFu >> (31u - (order & 31u))));
+  if (r == 0u || r > cn) return INVALID;
+  u32 k = O.sorted[seg.canon_base + r - 1u];
+  if (k >= cn) return INVALID;
+  Span sp = O.canon[seg.canon_base + k];
+  return order - sp.order < slen(sp) ? k : INVALID;
+}
 
 #define WAVES_PER_BLOCK 4
 
@@ -100,7 +119,7 @@ __global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const Do
   bcopy(dst.slot_of_leaf + w.leaf_base, src.slot_of_leaf + o.leaf_base, s.n_leaves);
   bcopy(dst.dir_leaf + w.blk_base * GROUP, src.dir_leaf + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
   bcopy(dst.dir_vis + w.blk_base * GROUP, src.dir_vis + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
-  if (w.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);
+  if (w.flags & o.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);
   bcopy(dst.cwo + w.cwo_base, src.cwo + o.cwo_base, s.n_cwo);
   bcopy(dst.dels + w.del_base, src.dels + o.del_base, s.n_del);
   bcopy(dst.dd + w.dd_base * DD_BLK, src.dd + o.dd_base * DD_BLK, (u64)s.n_ddb * DD_BLK);
@@ -118,6 +137,32 @@ __global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const Do
   }
   __syncthreads();
   if (threadIdx.x == 0) dst.st[d].n_agents = new_n_agents[d];
+}
+
+// Order -> leaf map of documents that start keeping it (their first remote stream after local
+// ones): INVALID everywhere, then every entry's orders -> its leaf, in directory order.  Block per
+// listed document; the barrier orders the two sweeps' stores.
+template <int L>
+__global__ __launch_bounds__(256) void k_build_map(Pools P, const u32* docs, u32 n) {
+  if (blockIdx.x >= n) return;
+  u32 d = docs[blockIdx.x];
+  DocState s = P.st[d];
+  DocSeg sg = P.seg[d];
+  u32* lof = P.leaf_of + sg.map_base;
+  for (u64 o = threadIdx.x; o < s.next_order; o += blockDim.x) lof[o] = INVALID;
+  __syncthreads();
+  const GroupRec* gr = P.groups + sg.grp_base;
+  const Span* lv = P.leaves + sg.leaf_base * L;
+  for (u32 g = 0; g < s.ng; g++) {
+    GroupRec G = gr[g];
+    for (u32 i = 0; i < G.cnt; i++) {
+      u32 leaf = P.dir_leaf[(sg.blk_base + G.blk) * GROUP + i];
+      for (u32 e = 0; e < (u32)L; e++) {
+        Span sp = lv[(u64)leaf * L + e];
+        for (u32 t = threadIdx.x; t < slen(sp); t += blockDim.x) lof[sp.order + t] = leaf;
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -146,12 +191,13 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   DocState s = w.ldT(P.st + d);
   DocSeg seg = w.ld_seg(P.seg + d);
   u32 l = lane_id();
-  if (s.status != ST_OK && s.status != ST_NEED_CAPACITY) {
+  if ((s.status != ST_OK && s.status != ST_NEED_CAPACITY) || s.next_order >= seg.ord_cap) {
     if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
     return;
   }
-  Span* canon = O.canon + seg.leaf_base * L;
-  u32* vpos = O.vpos + seg.leaf_base * L;
+  Span* canon = O.canon + seg.canon_base;
+  u32* vpos = O.vpos + seg.canon_base;
+  const u32 ccap = seg.canon_cap;  // (writes past it are dropped and reported below)
   const Span* leaves = P.leaves + seg.leaf_base * L;
   const GroupRec* groups = P.groups + seg.grp_base;  // the root level, read in order from HBM
   // Canonical spans, one leaf per step, lane i = entry i: an entry starts a new span unless
@@ -211,12 +257,12 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
       if (have && fs) open.len += (i32)rdlane(Pl, fs - 1u);
       if (M) {
         if (have) {
-          if (l == 0u) { canon[out] = open; vpos[out] = open_vpos; }
+          if (l == 0u && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
           out++;
         }
         u32 ls = 63u - (u32)__builtin_clzll(M);
         u32 rank = (u32)__popcll(M & ((1ull << l) - 1ull));
-        if (start && l != ls) {
+        if (start && l != ls && out + rank < ccap) {
           canon[out + rank] = Span{v.x, v.y, v.z, glen};
           vpos[out + rank] = vis + V - cl;
         }
@@ -229,44 +275,49 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
     }
   }
   if (have) {
-    if (l == 0) { canon[out] = open; vpos[out] = open_vpos; }
+    if (l == 0 && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
     out++;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  // order -> canonical span scatter.  Only item orders are written; delete orders keep whatever
-  // an earlier publish left there, so readers accept span_of[o] = k only if k < canon_n and
-  // canonical span k contains o (no span contains a delete order).  This saves a fill of
-  // 4 B x next_order per document.
-  u32* so = O.span_of + seg.map_base;
-  // 64 spans at a time, then 64 of their items at a time: item j finds its span m as (spans
-  // starting at or before the window's first item) + (span starts flagged in the window at or
-  // before j).  Span lanes flag their start in a 64-slot LDS row tagged with the window number
-  // (no clearing), item lanes read their slot, one ballot gives the start mask.  Item j of span
-  // m has order base_m + j, base = order - start.
-  u32 (*fl)[64] = s_flag;
-  u32 wv = uni(threadIdx.x >> 6);
-  fl[wv][l] = ~0u;
-  u32 tag = 0;
+  if (out > ccap) {  // canonical spans beyond the planned capacity: report, never write past it
+    if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  // Order -> canonical span index (replaces a 4 B/order table): a bitmap over the
+  // orders with a bit at every canonical span's first order, the exclusive count of set bits
+  // before every word, and the spans listed by first order.  Built in three sweeps: set the bits
+  // (atomic OR: spans are in document order, not order order), prefix-count the words (wave
+  // scans), scatter every span to its rank.  Per document 2 bits per order + 4 B per span are
+  // written instead of 4 B per item order.  Reads go through L2 (ld_l2): other lanes wrote them.
+  const u32 nw = pub_words(seg.ord_cap), used = s.next_order / 32u + 1u;
+  u32* bits = O.pub + seg.pub_base;
+  u32* pre = bits + nw;
+  u32* sorted = O.sorted + seg.canon_base;
+  for (u32 i = l; i < used; i += 64) bits[i] = 0u;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   u64 h = 0;
   for (u32 k0 = 0; k0 < out; k0 += 64) {
     u32 k = k0 + l;
-    Span sp = k < out ? canon[k] : Span{0, 0, 0, 0};
-    u32 ln = k < out ? slen(sp) : 0u;
-    if (k < out) h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
-    u32 Pi = wave_incl_scan(ln);
-    u32 T = rdlane(Pi, 63);
-    u32 st = Pi - ln;            // first item of span k within the chunk
-    u32 base = sp.order - st;
-    for (u32 t = 0; t < T; t += 64) {
-      ++tag;
-      if (k < out && st > t && st - t < 64u) fl[wv][st - t] = tag;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      u64 H = ballot(fl[wv][l] == tag);
-      u32 m = (u32)__popcll(ballot(k < out && st <= t)) - 1u + (u32)__popcll(H & ((2ull << l) - 1ull));
-      u32 bm = shfl(base, m);
-      u32 j = t + l;
-      if (j < T) so[bm + j] = k0 + m;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (k < out) {
+      Span sp = canon[k];
+      h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
+      atomicOr(bits + (sp.order >> 5), 1u << (sp.order & 31u));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  for (u32 i0 = 0, carry = 0; i0 < used; i0 += 64) {
+    u32 i = i0 + l;
+    u32 x = i < used ? (u32)__popc(ld_l2(bits + i)) : 0u;
+    u32 incl = wave_incl_scan(x);
+    if (i < used) pre[i] = carry + incl - x;
+    carry += rdlane(incl, 63);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  for (u32 k0 = 0; k0 < out; k0 += 64) {
+    u32 k = k0 + l;
+    if (k < out) {
+      u32 o = canon[k].order, wd = o >> 5;
+      sorted[ld_l2(pre + wd) + (u32)__popc(ld_l2(bits + wd) & ((1u << (o & 31u)) - 1u))] = k;
     }
   }
   const CwoRun* cwo = P.cwo + seg.cwo_base;
@@ -323,7 +374,7 @@ struct TextIO {
   const u32* content;  // order-indexed code points: document d reads content[cbase[d] + order]
   const u64* cbase;    // [doc] (NO_CONTENT: no content staged)
   const u64* clen;     // [doc] entries available from cbase
-  u32* text;           // [map_base + pos]
+  u32* text;           // [ord_base + pos]
   u32* tlen;           // [doc] visible chars written, INVALID if not materialised
   u64* tdigest;        // [doc] text digest (0 if not materialised)
 };
@@ -360,11 +411,11 @@ __global__ __launch_bounds__(64 * MAT_WAVES) void k_materialize(Pools P, PubOut 
     return;
   }
   DocSeg seg = P.seg[d];
-  const Span* cn = O.canon + seg.leaf_base * L;
-  const u32* vp = O.vpos + seg.leaf_base * L;
+  const Span* cn = O.canon + seg.canon_base;
+  const u32* vp = O.vpos + seg.canon_base;
   u32 ns = O.canon_n[d];
   const u32* src = T.content + cb;
-  u32* dst = T.text + seg.map_base;
+  u32* dst = T.text + seg.ord_base;
   constexpr u32 U = 4;
   // span of output position j: spans with visible items flag their first position in a 64-slot
   // LDS row per window (tag = step number, no clearing) together with base = order - start;
@@ -454,8 +505,8 @@ __global__ void k_pos_to_loc(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* d
       i32 stt = P.st[d].status;
       if ((stt == ST_OK || stt == ST_NEED_CAPACITY) && p < O.len[d]) {
         DocSeg seg = P.seg[d];
-        const u32* vp = O.vpos + seg.leaf_base * L;
-        const Span* cn = O.canon + seg.leaf_base * L;
+        const u32* vp = O.vpos + seg.canon_base;
+        const Span* cn = O.canon + seg.canon_base;
         u32 lo = 0, hi = O.canon_n[d];
         while (lo < hi) {
           u32 mid = (lo + hi) >> 1;
@@ -488,10 +539,10 @@ __global__ void k_loc_to_pos(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* d
         i32 r = find_run(ar, A.run_cnt, seq[q]);
         if (r >= 0) {
           u32 order = ar[r].order + (seq[q] - ar[r].key);
-          u32 k = O.span_of[seg.map_base + order];  // may be stale at a delete order (k_publish)
-          Span sp = k < O.canon_n[d] ? O.canon[seg.leaf_base * L + k] : Span{0, 0, 0, 0};
-          if (order - sp.order < slen(sp)) {
-            ps = O.vpos[seg.leaf_base * L + k] + (sp.len > 0 ? order - sp.order : 0u);
+          u32 k = span_of_order(O, seg, O.canon_n[d], order);
+          if (k != INVALID) {
+            Span sp = O.canon[seg.canon_base + k];
+            ps = O.vpos[seg.canon_base + k] + (sp.len > 0 ? order - sp.order : 0u);
             dl = sp.len < 0 ? 1 : 0;
           }
         }

@@ -69,7 +69,8 @@ enum : u32 {
   T_AGL_KEY, T_AGL_ORDER, T_AGL_LEN,
   T_RB_BASE,
   P_DDB,  // (2 slots) double-delete block directory
-  N_SLOTS = P_DDB + 2
+  P_PROBE = P_DDB + 2,  // (2 slots) probe answers
+  N_SLOTS = P_PROBE + 2
 };
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
 static_assert(S_PROF3 < K_FR, "DocState lives in the first context register");
@@ -103,6 +104,7 @@ struct Replayer {
   }
 #ifdef CRDT_PROF
   u32 prof_cat = 0;  // diagnostic: which fast path ran (0 typing, 2 delete, 3 insert)
+  u32 prof_mode = 0; // document d % 4: 0 cycles, 1 calls, 2 txns per path, 3 detail (below)
 #endif
 
   // ------------------------------------------------------------------ context access
@@ -137,6 +139,9 @@ struct Replayer {
   CRDT_HD u32 rec_n() const { return g(K_RECN); }
 
   CRDT_HD Replayer(const Pools& P, u32 d, const W& w0 = W()) : w(w0) {
+#ifdef CRDT_PROF
+    prof_mode = d & 3u;
+#endif
     DocSeg sg = w.ld_seg(P.seg + d);
     pset(P_LV, P.leaves + sg.leaf_base * (u64)L);
     pset(P_DL, P.dir_leaf + sg.blk_base * (u64)GROUP);
@@ -148,6 +153,7 @@ struct Replayer {
     pset(P_DELS, P.dels + sg.del_base);
     pset(P_DD, P.dd + sg.dd_base * (u64)DD_BLK);
     pset(P_DDB, P.ddb + sg.dd_base);
+    pset(P_PROBE, P.probe ? P.probe + sg.rec_base : nullptr);
     pset(P_TXNS, P.txns + sg.txn_base);
     pset(P_PAR, P.parents + sg.par_base);
     pset(P_FR, P.frontier + sg.fr_base);
@@ -156,7 +162,7 @@ struct Replayer {
     pset(P_RECS, P.recs + sg.rec_base);
     pset(P_STP, P.st + d);
     p(K_LEAF, sg.leaf_cap);
-    p(K_MAP, sg.map_cap);
+    p(K_MAP, (sg.flags & DOC_TRACK_MAP) ? sg.map_cap : INVALID);  // INVALID: no order -> leaf map
     p(K_CWO, sg.cwo_cap);
     p(K_TXN, sg.txn_cap);
     p(K_DEL, sg.del_cap);
@@ -375,7 +381,13 @@ struct Replayer {
   // leaf the run already lives in (INVALID for freshly inserted orders): no write if unchanged.
   CRDT_HD void notify(const Span& e, u32 leaf, u32 home) {
     if (home == leaf) return;
-    w.fill(lof() + e.order, slen(e), leaf);
+    map_fill(e.order, slen(e), leaf);
+  }
+  // Writes of the order -> leaf map, for documents that keep it (K_MAP != INVALID; the capacity
+  // checks against K_MAP then never trigger for the others).
+  CRDT_HD u32 tracked() const { return g(K_MAP) != INVALID; }
+  CRDT_HD void map_fill(u32 order, u32 n, u32 v) {
+    if (tracked()) w.fill(lof() + order, n, v);
   }
 
   // ------------------------------------------------------------------ cursor ops
@@ -464,6 +476,7 @@ struct Replayer {
       c = Cursor{cl, (u32)idx, order - w.cget_order((u32)idx)};
       return true;
     }
+    if (!tracked()) return false;  // (only remote ops look orders up: the host tracks their documents)
     u32 lf = w.ld(lof() + order);
     if (lf == INVALID || lf == cl) return false;
     if (load) {
@@ -501,7 +514,7 @@ struct Replayer {
     u32 stolen = w.cache_vis_from(idx);
     u32 first_moved = w.cget_order(idx);
     w.cache_write_moved(leafp(nl), idx, n, padding);
-    w.fill_runs(lof(), idx, n, nl);  // notify every moved entry
+    if (tracked()) w.fill_runs(lof(), idx, n, nl);  // notify every moved entry
     w.cache_clear(idx, n);
     p(C_NOW, g(C_NOW) - stolen);
     p(C_N, idx);
@@ -589,7 +602,13 @@ struct Replayer {
       bool follow = c.idx >= (u32)L / 2;
       u32 moved = cn - c.idx;
       u32 succ = g(C_SUCC), succ_ord = g(C_SUCC_ORD);  // the old leaf's successor follows nl
+#ifdef CRDT_PROF
+      u64 ts = w.clock();
+#endif
       u32 nl = split_at(c.idx, follow ? space : 0u);
+#ifdef CRDT_PROF
+      if (prof_mode == 3u) inc(S_PROF0, (u32)(w.clock() - ts));  // detail: split_at
+#endif
       if (follow) {  // the cursor follows the new leaf; its first `space` slots are padding
         u32 nblk = g(C_BLK), ni = g(C_I) + 1u;  // nl sits right after the old leaf
         commit();
@@ -662,6 +681,20 @@ struct Replayer {
     if (k < 0) return false;
     ARun r = w.ld_arun(ar + k);
     order = r.order + (seq - r.key);
+    return true;
+  }
+  CRDT_HD bool order_to_loc(u32 order, u32& agent, u32& seq) const {  // client_with_order.get() (simple_rle.rs:98-103)
+    u32 n = g(S_N_CWO), key = g(T_CWO_KEY);
+    if (n && order >= key && order - key < g(T_CWO_LEN)) {
+      agent = g(T_CWO_AGENT);
+      seq = g(T_CWO_SEQ) + (order - key);
+      return true;
+    }
+    i32 k = w.search_cwo(cwo(), n, order);
+    if (k < 0) return false;
+    CwoRun r = w.ld_cwo(cwo() + k);
+    agent = r.agent;
+    seq = r.seq + (order - r.key);
     return true;
   }
   CRDT_HD bool order_to_agent(u32 order, u32& agent) const {  // client_with_order.get()
@@ -984,7 +1017,7 @@ struct Replayer {
           if (del > 0) {
             if ((u64)lpos + del > cur_len()) return ST_POS_OOB;
             if (!cursor_at_content_pos(lpos, c)) return ST_POS_OOB;
-            w.fill(lof() + next, del, INVALID);  // delete orders name no item
+            map_fill(next, del, INVALID);  // delete orders name no item
             roll(c);                             // mutations.rs:539
             remaining = del;
             mode = M_LDEL;
@@ -1010,7 +1043,7 @@ struct Replayer {
             i32 st = id_to_order(op.w1 & 0xFFFFu, op.w2, target);
             if (st != ST_OK) return st;
             append_delete(next, target, len);  // doc.rs:305-308
-            w.fill(lof() + next, len, INVALID);
+            map_fill(next, len, INVALID);
             next += len;
             remaining = len;
             mode = M_RDEL;
@@ -1206,7 +1239,7 @@ struct Replayer {
     u32 total;
     u32 nt = typing_run(b0, nv, remote, agent, o.w1, o, total);
     if (g(K_MAP) - first < total) return 0;     // capacity: the general path stops exactly
-    w.fill(lof() + first, total, g(C_LEAF));   // notify (doc.rs:143-153)
+    map_fill(first, total, g(C_LEAF));   // notify (doc.rs:143-153)
     e.len += (i32)total;
     set(idx, e);
     inc(S_N_ITEMS, total);
@@ -1384,7 +1417,7 @@ struct Replayer {
     } else {
       append_delete(first, t1, done * l);  // forward deletes coalesce into one run (Rle::append)
     }
-    w.fill(lof() + first, done * l, INVALID);  // delete orders name no item
+    map_fill(first, done * l, INVALID);  // delete orders name no item
     fast_txn_commit(first, done * l);
     return done * per;
   }
@@ -1409,7 +1442,7 @@ struct Replayer {
     }
     p(C_N, n + space);
     inc(S_N_ENTRIES, space);
-    w.fill(lof() + item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
+    map_fill(item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
     set(idx + 1u, item);
     inc(S_N_ITEMS, len);
     return 1;
@@ -1510,6 +1543,40 @@ struct Replayer {
     return fast_deletes(b0, nv, remote, agent, idx, c.off, l, first, o);
   }
 
+  // PROBE record (config 1: check every position <-> CRDT location lookup as the replay goes): the
+  // README's two queries on the live state.  pos -> (agent, seq): the item at visible position
+  // q.w1 (root.rs:54-88 cursor_at_content_pos, cursor.rs:233-239 get_item, client_with_order.get);
+  // (agent, seq) -> (position, deleted): Cursor::count_pos (cursor.rs:147-190) of the item's cursor
+  // = visible items in the leaves before it (root level + directory block prefix) + in its leaf
+  // before it; deleted items report the position of the next visible one.  Unknown answers are
+  // (0xFFFF, 0xFFFFFFFF) and (0xFFFFFFFF, 2), as the published-index queries answer.
+  CRDT_HD void probe(const Rec& q, u32 pos) {
+    u32 a = 0xFFFFu, s = INVALID, ps = INVALID, dl = 2u;
+    Cursor c;
+    u32 o;
+    if (q.w1 < cur_len() && cursor_at_content_pos(q.w1, c) && get_item(c, o)) {
+      u32 a2, s2;
+      if (order_to_loc(o, a2, s2)) { a = a2; s = s2; }
+    }
+    if (q.w2 < g(S_N_AGENTS) && seq_to_order(q.w2, q.w3, o) && find_order(o, false, c)) {
+      commit();  // the directory's counts include the cached leaf's edits
+      u32 blk, i;
+      slot_of(c.leaf, blk, i);
+      u32 v = w.root_vis_before(w.root_find_blk(g(S_NG), blk)) + w.blk_vis_before(dvis(blk), i);
+      i32 el;
+      if (c.leaf == g(C_LEAF)) {
+        v += w.cache_vis_before(c.idx);
+        el = w.cget_len(c.idx);
+      } else {
+        v += w.peek_vis_before(leafp(c.leaf), c.idx, el);
+      }
+      ps = v + (el > 0 ? c.off : 0u);
+      dl = el < 0 ? 1u : 0u;
+    }
+    uint4* out = ptr<uint4>(P_PROBE);
+    if (out) w.st_probe(out + pos, a, s, ps, dl);
+  }
+
   // Replay this document's record stream from its rec_pos.  A GEN record stays current until
   // all its ops are applied (progress in S_GEN_DONE, so a capacity stop resumes mid-record).
   CRDT_HD void run() {
@@ -1538,8 +1605,11 @@ struct Replayer {
         u32 fast = fast_txn(pos, kind, gen, h, gop);
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
-        u32 dt = (u32)(t1 - t0);
-        if (!fast) inc(S_PROF1, dt);
+        u32 dt = prof_mode == 0u ? (u32)(t1 - t0) : prof_mode == 1u ? 1u : (fast ? fast / per_txn(kind == REC_RTXN || kind == REC_RC) : 0u);
+        if (prof_mode == 3u) {  // detail: fast ok / failed attempt
+          if (fast) inc(S_PROF3, (u32)(t1 - t0));
+          else inc(S_PROF2, (u32)(t1 - t0));
+        } else if (!fast) inc(S_PROF1, prof_mode == 0u ? dt : 0u);
         else if (prof_cat == 0u) inc(S_PROF0, dt);
         else if (prof_cat == 2u) inc(S_PROF2, dt);
         else inc(S_PROF3, dt);
@@ -1557,8 +1627,12 @@ struct Replayer {
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, inl, gop, gpar) : ST_BAD_INPUT;
         pre = 0;
 #ifdef CRDT_PROF
-        inc(S_PROF1, (u32)(w.clock() - t1));
+        inc(S_PROF1, (prof_mode == 0u || prof_mode == 3u) ? (u32)(w.clock() - t1) : 1u);  // detail: apply_txn
 #endif
+      } else if (kind == REC_PROBE) {
+        probe(h, pos);
+        st = ST_OK;
+        consumed = 1;
       } else {
         st = ST_BAD_INPUT;
         consumed = 1;

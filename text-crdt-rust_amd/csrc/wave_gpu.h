@@ -567,7 +567,31 @@ struct WaveGPU {
     return false;
   }
 
+  // visible items in the groups before g (probe: Cursor::count_pos)
+  __device__ __forceinline__ u32 root_vis_before(u32 g) const {
+    u32 l = lane_id(), t = 0;
+    for (u32 r = 0; r < g; r += 64) t += wave_sum(r + l < g ? (u32)rvis()[r + l] : 0u);
+    return t;
+  }
+
   // ---------------------------------------------------------------- directory blocks (HBM)
+  // visible items in the slots before i of a block row
+  __device__ __forceinline__ u32 blk_vis_before(const u32* dv, u32 i) const {
+    u32 l = lane_id();
+    u32 x = dv[l];  // 64-slot rows: always in bounds
+    return wave_sum(l < i ? x : 0u);
+  }
+  // visible items before entry idx of the cached leaf / of another leaf (+ that entry's length)
+  __device__ __forceinline__ u32 cache_vis_before(u32 idx) const { return wave_sum(lane_id() < idx ? clen_l() : 0u); }
+  __device__ __forceinline__ u32 peek_vis_before(const Span* p, u32 idx, i32& len_idx) const {
+    u32 l = lane_id();
+    i32 n = (i32)p[l & (u32)(L - 1)].len;
+    len_idx = (i32)rdlane((u32)n, idx);
+    return wave_sum(l < idx && l < (u32)L && n > 0 ? (u32)n : 0u);
+  }
+  __device__ __forceinline__ void st_probe(uint4* p, u32 a, u32 s, u32 ps, u32 dl) const {
+    *p = make_uint4(a, s, ps, dl);  // every lane stores the same values
+  }
   // slot of a block whose cumulative visible count first exceeds rem (+ its leaf id; both block
   // rows are loaded together so the descent costs one HBM round trip)
   __device__ __forceinline__ bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
