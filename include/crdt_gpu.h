@@ -188,6 +188,10 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
 // crdt_run + publish of it; a later reset + crdt_run_async replays it in exactly that room).
 // Capacities grow again on the next stage.  (Host-side planning; no reference counterpart.)
 int crdt_fit(crdt_engine* e);
+// on != 0: documents staged in one call from the same host stream (crdt_stage_local_shared,
+// crdt_stage_remote_replicated) read one device copy of it instead of a copy each (records
+// are read-only input).  Off by default.
+int crdt_set_share_streams(crdt_engine* e, int on);
 // Device bytes the engine holds (per-document pools, staged records, content, text).
 uint64_t crdt_mem_bytes(const crdt_engine* e);
 // Config 1's per-op check: after txn t (of every listed document), ask pos_to_loc(probes[t].pos)

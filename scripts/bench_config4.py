@@ -1,10 +1,13 @@
-"""Secondary measurement: BASELINE config 4 shape (random-edit documents generated on the device).
+"""Secondary measurement: BASELINE config 4 (random-edit documents; the per-GPU share of a
+1M-document corpus: 125,000 documents per MI355X).
 
 Each document replays `--ops` local txns drawn inside the replay wave from one GEN record
-(make_random_change semantics, doc.rs:544-569).  One step = reset + replay + publish.  Prints one
-JSON line.  Not the driver's bench (bench.py is); the CPU leg replays a bounded sample of the same
-documents with the oracle (test infrastructure, used only as the baseline)."""
+(make_random_change semantics, doc.rs:544-569; no input records per op).  One step = reset +
+replay + publish.  Parity: the digests of a sampled subset of documents equal the oracle's
+replay of the same generated ops (the oracle is the checker here, and the CPU baseline).  Prints
+one JSON line (bench.py stays the driver's bench)."""
 import argparse
+import ctypes as C
 import json
 import os
 import sys
@@ -17,57 +20,83 @@ sys.path.insert(0, os.path.join(ROOT, "text-crdt-rust_amd"))
 sys.path.insert(0, ROOT)
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--docs", type=int, default=32768)
+ap.add_argument("--docs", type=int, default=125000)
 ap.add_argument("--ops", type=int, default=20000)
-ap.add_argument("--steps", type=int, default=3)
+ap.add_argument("--steps", type=int, default=2)
 ap.add_argument("--seed", type=int, default=0xC0FFEE)
-ap.add_argument("--cpu-docs", type=int, default=64)
+ap.add_argument("--check-docs", type=int, default=64, help="documents checked against the oracle")
 a = ap.parse_args()
 
 import crdt_amd  # noqa: E402
-from bench import splitmix64  # noqa: E402
+from bench import splitmix64, cpu_share, SIMDS  # noqa: E402
 
 e = crdt_amd.Engine(a.docs, 32)
 t0 = time.time()
 e.stage_random(list(range(a.docs)), "gen", a.ops, a.seed)
-st = e.run()  # untimed: capacity growth
+st = e.run()  # untimed: capacity growth, index sizing
 assert (st == 0).all(), np.unique(st)
 e.publish_async()
 e.sync()
 dg0 = e.digests().copy()
-ts, rms = [], []
+stage_s = time.time() - t0
+mem = e.mem_bytes()
+hip = C.CDLL("libamdhip64.so")
+ev = [C.c_void_p() for _ in range(3)]
+for x in ev:
+    hip.hipEventCreate(C.byref(x))
+s_ = C.c_void_p(e.stream())
+ts, rms, pms = [], [], []
 for _ in range(a.steps):
     e.sync()
     t1 = time.perf_counter()
     e.reset_async()
+    hip.hipEventRecord(ev[0], s_)
     e.run_async()
+    hip.hipEventRecord(ev[1], s_)
     e.publish_async()
+    hip.hipEventRecord(ev[2], s_)
     e.sync()
     ts.append(time.perf_counter() - t1)
-    rms.append(e.timings()[0])
+    x, y = C.c_float(), C.c_float()
+    hip.hipEventElapsedTime(C.byref(x), ev[0], ev[1])
+    hip.hipEventElapsedTime(C.byref(y), ev[1], ev[2])
+    rms.append(x.value)
+    pms.append(y.value)
 ok = bool((e.status() == 0).all()) and bool((e.digests() == dg0).all())
-# CPU leg: the oracle on a sample of the same documents (one thread per doc via a pool of 16)
+# parity on a sample + the CPU baseline: the oracle on sampled documents, every host core
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from concurrent.futures import ThreadPoolExecutor  # noqa: E402
 from oracle_lib import OracleDoc  # noqa: E402
 
+rng = np.random.default_rng(7)
+check = sorted(set(rng.integers(0, a.docs, a.check_docs).tolist()) | {0, a.docs - 1})
+
 
 def one(d):
-    o = OracleDoc()
+    o = OracleDoc(32, 16, split_index=True)
     assert o.apply_random(o.agent("gen"), a.ops, splitmix64(a.seed ^ d) & 0xFFFFFFFF) == 0
     return o.digest()
 
 
+threads, affinity, quota = cpu_share()
 c0 = time.perf_counter()
-with ThreadPoolExecutor(16) as ex:
-    cdg = list(ex.map(one, range(a.cpu_docs)))
+with ThreadPoolExecutor(threads) as ex:
+    cdg = list(ex.map(one, check))
 csec = time.perf_counter() - c0
-ok = ok and all(int(dg0[d]) == cdg[d] for d in range(a.cpu_docs))
+ok = ok and all(int(dg0[d]) == g for d, g in zip(check, cdg))
 t = min(ts)
 print(json.dumps({
     "metric": "CRDT ops remapped+merged/sec (config 4: on-device random edits)", "value": a.docs * a.ops / t,
-    "unit": "ops/s", "docs": a.docs, "ops_per_doc": a.ops, "ms_per_step": t * 1e3,
-    "cpu_sample": {"docs": a.cpu_docs, "threads": 16, "ops_per_s": a.cpu_docs * a.ops / csec,
-                   "note": "oracle C++ restatement via ctypes threads (GIL released in C)"},
-    "parity_ok": ok, "stage_s": time.time() - t0 - sum(ts) - csec,
+    "unit": "ops/s", "n_gpus": 1, "steps": a.steps, "ms_per_step": t * 1e3, "higher_is_better": True,
+    "dtype": "u32", "data": "synthetic: make_random_change semantics generated in the replay wave",
+    "config": {"workload": f"config4: {a.docs} docs/GPU (1M docs / 8 GPUs) x {a.ops} random ops, replay+publish",
+               "docs_per_gpu": a.docs, "ops_per_doc": a.ops, "waves_per_simd": a.docs / SIMDS,
+               "hbm_bytes_per_doc": mem / a.docs, "hbm_bytes": mem},
+    "kernels_ms": {"k_replay": float(np.mean(rms)), "k_publish": float(np.mean(pms))},
+    "cpu_baseline": {"value": len(check) * a.ops / csec, "unit": "ops/s", "threads_used": threads,
+                     "host_cores": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
+                     "kind": "port", "sample": f"{len(check)} docs on the oracle (SplitList index), ctypes threads "
+                                               f"(GIL released in C), {csec:.1f} s"},
+    "parity_ok": ok, "parity": f"{len(check)} sampled documents' digests == oracle; every step's digests equal",
+    "stage_s": stage_s,
 }))

@@ -59,15 +59,10 @@ struct PoolSet {
   u32* frontier = nullptr;
   GroupRec* groups = nullptr;
   AgentRec* agents = nullptr;
-  Span* canon = nullptr;
-  u32* vpos = nullptr;
-  u32* sorted = nullptr;
-  u32* pub = nullptr;
   u64 bytes = 0;
   void free_all() {
     dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(cwo); dfree(arun);
-    dfree(dels); dfree(dd); dfree(ddb); dfree(txns); dfree(parents); dfree(frontier); dfree(groups); dfree(agents); dfree(canon);
-    dfree(vpos); dfree(sorted); dfree(pub);
+    dfree(dels); dfree(dd); dfree(ddb); dfree(txns); dfree(parents); dfree(frontier); dfree(groups); dfree(agents);
     bytes = 0;
   }
 };
@@ -88,6 +83,7 @@ inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
   for (size_t a = 0; a < n.txns_per_agent.size(); a++) c.txns_per_agent[a] += n.txns_per_agent[a];
   c.txn_max(n.max_ops, n.max_del, n.max_len, n.max_parents);
   c.probes += n.probes;
+  c.local_del_ops += n.local_del_ops;
 }
 
 // Launch shape of a wave-per-document kernel whose waves hold an LDS root of `rcap` groups:
@@ -134,6 +130,7 @@ struct crdt_engine {
   uint4* probe = nullptr;  // PROBE answers, one slot per staged record (when probes are staged)
   u64 probe_cap = 0;
   bool has_probes = false;
+  bool share_streams = false;  // documents staged with the same host stream read one device copy
   bool published = false;
   double last_replay_ms = 0, last_publish_ms = 0, last_materialize_ms = 0;
   // text materialisation: order-indexed content streams, per-document stream offsets, output text
@@ -145,6 +142,14 @@ struct crdt_engine {
   u32* text = nullptr;
   u64 text_cap = 0;
   u64 ord_total = 0;  // text buffer entries (sum of ord_cap)
+  // published index (k_publish output, no state: re-sized without copying, see size_pub)
+  Span* canon = nullptr;
+  u32* vpos = nullptr;
+  u32* sorted = nullptr;
+  u32* pub = nullptr;
+  u64 canon_alloc = 0, pub_alloc = 0;
+  bool pub_sized = false;   // the index pools fit the device state (else publish sizes them first)
+  bool pub_fitted = false;  // crdt_fit sized them for the staged stream (replays need no check)
   u32* tlen = nullptr;
   u64* tdigest = nullptr;
   bool materialized = false;
@@ -177,10 +182,10 @@ struct crdt_engine {
   }
   PubOut pub_view() const {
     PubOut o{};
-    o.canon = pools.canon;
-    o.vpos = pools.vpos;
-    o.sorted = pools.sorted;
-    o.pub = pools.pub;
+    o.canon = canon;
+    o.vpos = vpos;
+    o.sorted = sorted;
+    o.pub = pub;
     o.canon_n = canon_n;
     o.len = len;
     o.digest = digest;
@@ -189,6 +194,9 @@ struct crdt_engine {
 
   void release() {
     pools.free_all();
+    dfree(canon); dfree(vpos); dfree(sorted); dfree(pub);
+    canon_alloc = pub_alloc = 0;
+    pub_sized = pub_fitted = false;
     dfree(st); dfree(segs); dfree(canon_n); dfree(len); dfree(digest); dfree(n_agents_d); dfree(doc_list);
     n_agents_pushed.clear();
     classes.clear();
@@ -248,7 +256,6 @@ struct crdt_engine {
     int r = 0;
     PoolSet np;
     u64 nl = 0, nb = 0, nm = 0, nc = 0, na = 0, ndl = 0, ndd = 0, nt = 0, npar = 0, nag = 0, nfr = 0;
-    u64 ncan = 0, npub = 0, nord = 0;
     std::vector<DocSeg> nseg(n_docs);
     std::vector<AgentRec> agent_tab;
     std::vector<u32> n_agents(n_docs);
@@ -265,11 +272,8 @@ struct crdt_engine {
       s.txn_base = nt; s.txn_cap = c.txn; nt += c.txn;
       s.par_base = npar; s.par_cap = c.par; npar += c.par;
       s.fr_base = nfr; s.fr_cap = c.fr; nfr += c.fr;
-      s.canon_cap = c.canon ? c.canon : (u32)std::min<u64>((u64)c.leaf * L, 0xFFFFFFFFull);
-      s.canon_base = ncan; ncan += s.canon_cap;
-      s.ord_cap = std::max<u32>(c.ord, 1u);
-      s.ord_base = nord; nord += s.ord_cap;
-      s.pub_base = npub; npub += 2ull * pub_words(s.ord_cap);
+      s.canon_base = seg_h[d].canon_base; s.canon_cap = seg_h[d].canon_cap;  // (size_pub's)
+      s.pub_base = seg_h[d].pub_base; s.ord_base = seg_h[d].ord_base; s.ord_cap = seg_h[d].ord_cap;
       s.grp_base = s.blk_base; s.grp_cap = c.blk;  // one root group per directory block
       s.agent_base = nag;
       u32 ag = (u32)h.agents.names.size();
@@ -309,11 +313,7 @@ struct crdt_engine {
     HIPCHK(dalloc(np.frontier, nfr));
     HIPCHK(dalloc(np.groups, nb));
     HIPCHK(dalloc(np.agents, nag));
-    HIPCHK(dalloc(np.canon, ncan));
-    HIPCHK(dalloc(np.vpos, ncan));
-    HIPCHK(dalloc(np.sorted, ncan));
-    HIPCHK(dalloc(np.pub, npub));
-    np.bytes = nl * L * 16 + ncan * 24 + npub * 4 + nl * 4 + nb * GROUP * 8 + nm * 4 + nc * 16 + na * 16 + ndl * 12 +
+    np.bytes = nl * L * 16 + nl * 4 + nb * GROUP * 8 + nm * 4 + nc * 16 + na * 16 + ndl * 12 +
                ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * 16 + nfr * 4 + nb * 16;
     if (!agent_tab.empty())
       HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
@@ -339,9 +339,47 @@ struct crdt_engine {
     seg_h = nseg;
     r = plan_classes();
     if (r) return r;
-    ord_total = nord;
+    pub_sized = false;
     published = false;
     materialized = false;
+    return 0;
+  }
+
+  // Size the published-index pools for the documents' current state: canonical spans <= the
+  // state's leaf entries (or crdt_fit's exact count), orders < ord_cap.  Outputs only, so the
+  // pools are freed before the new ones are allocated (no copy, no double footprint).
+  int size_pub() {
+    int r = pull_states();
+    if (r) return r;
+    u64 ncan = 0, npub = 0, nord = 0;
+    for (u64 d = 0; d < n_docs; d++) {
+      DocSeg& s = seg_h[d];
+      Caps& c = docs[d].caps;
+      if (st_h[d].next_order >= c.ord) c.ord = st_h[d].next_order + 1;
+      s.canon_cap = std::max<u32>(c.canon ? c.canon : st_h[d].n_entries, 1u);
+      s.canon_base = ncan; ncan += s.canon_cap;
+      s.ord_cap = std::max<u32>(c.ord, 1u);
+      s.ord_base = nord; nord += s.ord_cap;
+      s.pub_base = npub; npub += 2ull * pub_words(s.ord_cap);
+    }
+    if (ncan > canon_alloc || ncan < canon_alloc / 2) {
+      dfree(canon); dfree(vpos); dfree(sorted);
+      canon_alloc = 0;
+      HIPCHK(dalloc(canon, ncan));
+      HIPCHK(dalloc(vpos, ncan));
+      HIPCHK(dalloc(sorted, ncan));
+      canon_alloc = ncan;
+    }
+    if (npub > pub_alloc || npub < pub_alloc / 2) {
+      dfree(pub);
+      pub_alloc = 0;
+      HIPCHK(dalloc(pub, npub));
+      pub_alloc = npub;
+    }
+    ord_total = nord;
+    HIPCHK(hipMemcpyAsync(segs, seg_h.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    pub_sized = true;
     return 0;
   }
 
@@ -457,6 +495,7 @@ struct crdt_engine {
       StreamNeeds& c = h.cum;
       add_needs(c, needs[i]);
       h.staged = needs[i];
+      pub_fitted = false;
       Caps nc = plan_caps(c, (u32)h.agents.names.size(), h.tracked, 48);
       Caps& oc = h.caps;
       auto up = [&](u32& o, u32 v) { if (v > o) { o = v; grow = true; } };
@@ -474,8 +513,13 @@ struct crdt_engine {
     }
     // records: one buffer for this call
     u64 total = 0, n_probes = 0;
-    for (auto* s : streams) total += s->size();
     for (auto& n : needs) n_probes += n.probes;
+    bool share = share_streams && n_probes == 0;  // (probe answers are per record slot)
+    {
+      std::unordered_map<const std::vector<Rec>*, char> seen;
+      for (auto* s : streams)
+        if (!share || seen.emplace(s, 1).second) total += s->size();
+    }
     if (total > rec_cap) {
       dfree(recs);
       rec_cap = std::max<u64>(total, 1024);
@@ -509,6 +553,10 @@ struct crdt_engine {
       sg.rec_base = off;
       sg.rec_n = (u32)sv.size();
       auto up = uploaded.find(&sv);
+      if (share && up != uploaded.end()) {  // read-only input: reference the first copy
+        sg.rec_base = up->second;
+        continue;
+      }
       if (!sv.empty()) {
         if (&sv == prev || up != uploaded.end()) {
           r = flush();
@@ -572,6 +620,7 @@ struct crdt_engine {
       else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
       HIPCHK(hipGetLastError());
     }
+    if (!pub_fitted) pub_sized = false;  // the state grows: size the index again before publishing
     published = false;
     materialized = false;
     return 0;
@@ -625,18 +674,9 @@ struct crdt_engine {
       r = layout(true);
       if (r) return r;
     }
-    // the published index and the text need room for every order (the estimate can be short for
-    // generated streams, and documents without the order map never stop for it)
-    bool grow_ord = false;
-    for (u64 d = 0; d < n_docs; d++)
-      if (st_h[d].next_order >= seg_h[d].ord_cap) {
-        docs[d].caps.ord = st_h[d].next_order + 1;
-        grow_ord = true;
-      }
-    if (grow_ord) {
-      r = layout(true);
-      if (r) return r;
-    }
+    // the published index (and the text) for this state: sized now, while the stream is idle
+    r = size_pub();
+    if (r) return r;
     if (status_out)
       for (u64 d = 0; d < n_docs; d++) status_out[d] = st_h[d].status == ST_NEED_CAPACITY ? ST_CAPACITY : st_h[d].status;
     return 0;
@@ -669,7 +709,12 @@ struct crdt_engine {
       c.canon = std::max<u32>(cn[d], 1);
       c.fr = std::max<u32>(s.n_fr + 1, FRONTIER_CAP0);
     }
-    return layout(true);
+    r = layout(true);
+    if (r) return r;
+    r = size_pub();
+    if (r) return r;
+    pub_fitted = true;  // replays of the staged streams publish exactly this much
+    return 0;
   }
 
   int publish() {
@@ -677,6 +722,10 @@ struct crdt_engine {
     if (r) return r;
     u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     if (!n_docs) return 0;
+    if (!pub_sized) {  // (waits for the replay in flight: the index is sized from its state)
+      r = size_pub();
+      if (r) return r;
+    }
     HIPCHK(hipEventRecord(ev[2], stream));
     if (L == 32) hipLaunchKernelGGL(k_publish<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
     else hipLaunchKernelGGL(k_publish<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
@@ -1096,6 +1145,12 @@ int crdt_apply_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs
   return 0;
 }
 
+int crdt_set_share_streams(crdt_engine* e, int on) {
+  if (!e) return CRDT_E_ARG;
+  e->share_streams = on != 0;
+  return 0;
+}
+
 int crdt_fit(crdt_engine* e) {
   if (!valid(e)) return CRDT_E_ARG;
   int r = e->set_device();
@@ -1253,7 +1308,7 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
         li++;
       }
   }
-  if (canon4 && s[2]) HIPCHK(hipMemcpy(canon4, e->pools.canon + sg.canon_base, s[2] * 16, hipMemcpyDeviceToHost));
+  if (canon4 && s[2]) HIPCHK(hipMemcpy(canon4, e->canon + sg.canon_base, s[2] * 16, hipMemcpyDeviceToHost));
   if (cwo4 && st.n_cwo) HIPCHK(hipMemcpy(cwo4, e->pools.cwo + sg.cwo_base, st.n_cwo * 16, hipMemcpyDeviceToHost));
   if (del3 && st.n_del) HIPCHK(hipMemcpy(del3, e->pools.dels + sg.del_base, st.n_del * 12, hipMemcpyDeviceToHost));
   if (dd3 && st.n_dd) {  // flatten the blocks in directory order
@@ -1289,7 +1344,8 @@ int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23) {
 
 uint64_t crdt_mem_bytes(const crdt_engine* e) {
   if (!e) return 0;
-  return e->pools.bytes + e->rec_cap * sizeof(Rec) + e->content_cap * 4 + e->text_cap * 4 +
+  return e->pools.bytes + e->rec_cap * sizeof(Rec) + e->content_cap * 4 + e->text_cap * 4 + e->canon_alloc * 24 +
+         e->pub_alloc * 4 + e->probe_cap * 16 +
          e->n_docs * (sizeof(DocState) + sizeof(DocSeg) + 4 + 4 + 8);
 }
 

@@ -99,6 +99,7 @@ struct StreamNeeds {
   // largest single txn (the replay checks room for one txn before applying it)
   u32 max_ops = 0, max_del = 0, max_len = 0, max_parents = 0;
   u64 probes = 0;  // PROBE records (their documents keep the order -> leaf map)
+  u64 local_del_ops = 0;  // LocalOps that delete
   std::vector<u32> txns_per_agent;
   void txn_max(u32 ops, u64 del, u64 len, u32 parents) {
     max_ops = std::max(max_ops, ops);
@@ -123,11 +124,13 @@ inline void encode_local_txn(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, 
   if (nops == 1 && agent <= 0xFFFFu && span <= 0xFFFFFFFFull) {  // one LocalOp: one compact record
     out.push_back(Rec{(REC_LC << 28) | agent, ops3[0], ops3[1], ops3[2]});
     nd.local_del += ops3[1];
+    nd.local_del_ops += ops3[1] != 0;
   } else {
     out.push_back(Rec{(REC_LTXN << 28) | (nops & 0x0FFFFFFFu), agent, dels32, span32});
     for (u32 k = 0; k < nops; k++) {
       out.push_back(Rec{REC_LOP << 28, ops3[3 * k], ops3[3 * k + 1], ops3[3 * k + 2]});
       nd.local_del += ops3[3 * k + 1];
+      nd.local_del_ops += ops3[3 * k + 1] != 0;
     }
   }
   nd.n_txn++;
@@ -227,6 +230,7 @@ inline void encode_gen(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, u32 n_
   nd.n_ops += n_ops;
   nd.orders += 3ull * n_ops;
   nd.local_del += n_ops;
+  nd.local_del_ops += n_ops;
   if (agent < 0xFFFE) {
     if (nd.txns_per_agent.size() <= agent) nd.txns_per_agent.resize(agent + 1, 0);
     nd.txns_per_agent[agent] += n_ops;
@@ -266,7 +270,10 @@ inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_
   u64 arun = 0;
   for (u32 a = 0; a < n_agents; a++) arun += (a < nd.txns_per_agent.size() ? nd.txns_per_agent[a] : 0) + 1;
   c.arun = (u32)arun;
-  c.del = (u32)std::min<u64>(nd.local_del + nd.remote_del_ops + 1, 0xFFFFFFFFull);
+  // delete runs: at most one per deleted item, usually one or two per delete op (a table that
+  // fills stops its document resumably and grows)
+  c.del = (u32)std::min<u64>(std::min<u64>(nd.local_del + nd.remote_del_ops, 2 * (nd.local_del_ops + nd.remote_del_ops) + 64) + 1,
+                             0xFFFFFFFFull);
   c.dd = nd.remote_del_ops ? 4u : 0u;  // double-delete blocks: grown on demand (rare but for config 5)
   c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + 64 + 1, 1024 + (nd.remote_parents + nd.n_txn) / 64);
   c.agent = n_agents;

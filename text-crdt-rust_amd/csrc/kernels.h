@@ -26,7 +26,11 @@ struct PubOut {
 // Order -> canonical span through the published index: r = span starts at or below `order`;
 // the span is sorted[r - 1] if it contains the order (delete orders lie in no span).  Returns
 // the span index or INVALID.
+#ifdef PUB_PLAIN_LOADS
+__device__ __forceinline__ u32 ld_l2(const u32* p) { return *p; }
+#else
 __device__ __forceinline__ u32 ld_l2(const u32* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+#endif
 __device__ __forceinline__ u32 span_of_order(const PubOut& O, const DocSeg& seg, u32 cn, u32 order) {
   u32 nw = pub_words(seg.ord_cap);
   const u32* bits = O.pub + seg.pub_base;
@@ -289,7 +293,11 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   // (atomic OR: spans are in document order, not order order), prefix-count the words (wave
   // scans), scatter every span to its rank.  Per document 2 bits per order + 4 B per span are
   // written instead of 4 B per item order.  Reads go through L2 (ld_l2): other lanes wrote them.
+#ifdef PUB_NO_INDEX
+  const u32 nw = pub_words(seg.ord_cap), used = 0u;
+#else
   const u32 nw = pub_words(seg.ord_cap), used = s.next_order / 32u + 1u;
+#endif
   u32* bits = O.pub + seg.pub_base;
   u32* pre = bits + nw;
   u32* sorted = O.sorted + seg.canon_base;
@@ -298,28 +306,59 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   u64 h = 0;
   for (u32 k0 = 0; k0 < out; k0 += 64) {
     u32 k = k0 + l;
-    if (k < out) {
-      Span sp = canon[k];
-      h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
-      atomicOr(bits + (sp.order >> 5), 1u << (sp.order & 31u));
+    Span sp = k < out ? canon[k] : Span{0, 0, 0, 0};
+    if (k < out) h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
+#ifndef PUB_NO_INDEX
+    // nearby spans share bitmap words: OR each distinct word's bits across the wave first, then
+    // one atomic per word (same-address atomics serialise at L2)
+    u32 wd = sp.order >> 5, bit = 1u << (sp.order & 31u);
+    for (u64 todo = ballot(k < out); todo;) {
+      u32 wl = rdlane(wd, (u32)__builtin_ctzll(todo));
+      u64 m = ballot(k < out && wd == wl);
+      u32 word = wave_or((m >> l) & 1u ? bit : 0u);
+      if (l == (u32)__builtin_ctzll(m)) atomicOr(bits + wl, word);
+      todo &= ~m;
+    }
+#endif
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  // (4 steps per iteration: their loads are in flight together)
+  for (u32 i0 = 0, carry = 0; i0 < used; i0 += 256) {
+    u32 x[4];
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) {
+      u32 i = i0 + 64 * u + l;
+      x[u] = i < used ? (u32)__popc(ld_l2(bits + i)) : 0u;
+    }
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) {
+      u32 i = i0 + 64 * u + l;
+      u32 incl = wave_incl_scan(x[u]);
+      if (i < used) pre[i] = carry + incl - x[u];
+      carry += rdlane(incl, 63);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  for (u32 i0 = 0, carry = 0; i0 < used; i0 += 64) {
-    u32 i = i0 + l;
-    u32 x = i < used ? (u32)__popc(ld_l2(bits + i)) : 0u;
-    u32 incl = wave_incl_scan(x);
-    if (i < used) pre[i] = carry + incl - x;
-    carry += rdlane(incl, 63);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  for (u32 k0 = 0; k0 < out; k0 += 64) {
-    u32 k = k0 + l;
-    if (k < out) {
-      u32 o = canon[k].order, wd = o >> 5;
-      sorted[ld_l2(pre + wd) + (u32)__popc(ld_l2(bits + wd) & ((1u << (o & 31u)) - 1u))] = k;
+#ifndef PUB_NO_INDEX
+  for (u32 k0 = 0; k0 < out; k0 += 256) {
+    u32 o[4], r[4];
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) {
+      u32 k = k0 + 64 * u + l;
+      o[u] = k < out ? canon[k].order : 0u;
+    }
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) {
+      u32 wd = o[u] >> 5;
+      r[u] = ld_l2(pre + wd) + (u32)__popc(ld_l2(bits + wd) & ((1u << (o[u] & 31u)) - 1u));
+    }
+#pragma unroll
+    for (u32 u = 0; u < 4; u++) {
+      u32 k = k0 + 64 * u + l;
+      if (k < out) sorted[r[u]] = k;
     }
   }
+#endif
   const CwoRun* cwo = P.cwo + seg.cwo_base;
   for (u32 k = l; k < s.n_cwo; k += 64) {
     CwoRun r = cwo[k];

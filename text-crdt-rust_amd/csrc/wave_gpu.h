@@ -28,6 +28,16 @@ __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
   return v;
 }
 __device__ __forceinline__ u32 wave_sum(u32 v) { return rdlane(wave_incl_scan(v), 63); }
+// OR over the wave (the same DPP sequence with |)
+__device__ __forceinline__ u32 wave_or(u32 v) {
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);
+  v |= __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);
+  return rdlane(v, 63);
+}
 
 template <int L>
 struct WaveGPU {
