@@ -332,6 +332,36 @@ double orc_cpu_baseline_local(uint32_t ndocs, uint32_t threads, uint32_t ntxn, c
   return t1 - t0;
 }
 
+// Config 4 on host cores: document i replays n_ops generated local txns (random_change, seed
+// seeds[i]) on `threads` threads, one document per task (split_index: SplitList order index).
+double orc_cpu_baseline_random(uint32_t ndocs, uint32_t threads, uint32_t n_ops, const uint32_t* seeds,
+                               uint64_t* checksum, int split_index) {
+  std::atomic<uint32_t> next{0};
+  std::atomic<uint64_t> sum{0};
+  auto worker = [&]() {
+    uint64_t local = 0;
+    while (true) {
+      uint32_t i = next.fetch_add(1);
+      if (i >= ndocs) break;
+      Doc d(32, 16, true, split_index != 0);
+      u16 a = d.get_or_create_agent_id("gen");
+      for (uint32_t k = 0; k < n_ops; k++) {
+        LocalOp op = random_change(seeds[i], k, d.len());
+        if (d.apply_local_txn(a, &op, 1) != OK) break;
+      }
+      local += d.len() + (uint64_t)d.status;
+    }
+    sum += local;
+  };
+  double t0 = now_s();
+  std::vector<std::thread> ts;
+  for (uint32_t k = 0; k < threads; k++) ts.emplace_back(worker);
+  for (auto& t : ts) t.join();
+  double t1 = now_s();
+  if (checksum) *checksum = sum.load();
+  return t1 - t0;
+}
+
 // Remote replay of a wire batch for `ndocs` documents (the reference takes &RemoteTxn, so each
 // worker materialises the RemoteTxn list once, before the timed region, with document i's name at
 // index `rename_idx` replaced by names[i] for the first document it owns; names never change the

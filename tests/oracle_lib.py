@@ -55,6 +55,8 @@ def lib():
     L.orc_stats.argtypes = [vp, P(u64)]
     L.orc_text.argtypes = [vp, P(u32), u64, P(u32), u64, P(u64)]
     L.orc_text.restype = i64
+    L.orc_cpu_baseline_random.argtypes = [u32, u32, u32, P(u32), P(u64), C.c_int]
+    L.orc_cpu_baseline_random.restype = C.c_double
     L.orc_probe_trace.argtypes = [vp, u16, u32, P(u32), P(u32), P(u32), P(u32)]
     L.orc_dd_new.restype = vp
     L.orc_dd_free.argtypes = [vp]

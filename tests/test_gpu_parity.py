@@ -328,3 +328,31 @@ def test_config1_every_op_probed(L):
         oans = np.concatenate(oans)
         bad = np.argwhere((ans != oans).any(1))
         assert bad.size == 0, (int(bad[0][0]), ans[bad[0][0]], oans[bad[0][0]])
+
+
+def test_long_document_publish_chains():
+    # Documents with >= 2048 leaves publish with a workgroup each (k_publish_big): the leaf
+    # sequence is cut into 16 ranges and canonical spans crossing range boundaries are joined.
+    # Forward-deleting a typed run leaves one deleted entry per item (split over thousands of
+    # leaves) that all coalesce into ONE canonical span crossing every range; a second document
+    # keeps a visible head and tail around the deleted middle.
+    n = 200_000
+    full = [(0, 0, n)] + [(0, 1, 0)] * n
+    part = [(0, 0, n)] + [(1000, 1, 0)] * (n // 2) + [(n // 2, 0, 7)]
+    for L in (32, 4):
+        e = crdt_amd.Engine(2, L)
+        ag = e.agent_intern([0, 1], ["f", "f"])
+        per = [full, part]
+        tx = np.concatenate([np.stack([np.full(len(t), ag[i]), np.ones(len(t))], 1) for i, t in enumerate(per)])
+        st = e.apply_local_arrays([0, 1], [0, len(full), len(full) + len(part)], tx, np.concatenate([np.array(t) for t in per]))
+        assert (st == 0).all(), st
+        for i, ops in enumerate(per):
+            o = OracleDoc(L, 16 if L == 32 else 8)
+            a = o.agent("f")
+            c = np.ones(len(ops), np.uint32)
+            assert o.apply_trace(a, c, np.array(ops, np.uint32)) == 0
+            assert o.sizes()["leaves"] >= 2048
+            assert_same(e.export(i), o.export())
+            assert int(e.digests()[i]) == o.digest()
+            check_queries_sampled(e, i, o, n=1 << 14)
+        assert e.export(0)["canon"].shape[0] <= 2

@@ -150,6 +150,9 @@ struct crdt_engine {
   u64 canon_alloc = 0, pub_alloc = 0;
   bool pub_sized = false;   // the index pools fit the device state (else publish sizes them first)
   bool pub_fitted = false;  // crdt_fit sized them for the staged stream (replays need no check)
+  // publish launches: documents with >= PUB_BIG_MIN leaves get a workgroup each (k_publish_big)
+  std::vector<u32> pub_small, pub_big;
+  u32* pub_list = nullptr;  // [small docs..., big docs...] when there are big ones
   u32* tlen = nullptr;
   u64* tdigest = nullptr;
   bool materialized = false;
@@ -194,7 +197,9 @@ struct crdt_engine {
 
   void release() {
     pools.free_all();
-    dfree(canon); dfree(vpos); dfree(sorted); dfree(pub);
+    dfree(canon); dfree(vpos); dfree(sorted); dfree(pub); dfree(pub_list);
+    pub_small.clear();
+    pub_big.clear();
     canon_alloc = pub_alloc = 0;
     pub_sized = pub_fitted = false;
     dfree(st); dfree(segs); dfree(canon_n); dfree(len); dfree(digest); dfree(n_agents_d); dfree(doc_list);
@@ -378,6 +383,23 @@ struct crdt_engine {
     }
     ord_total = nord;
     HIPCHK(hipMemcpyAsync(segs, seg_h.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
+    // long documents publish with a workgroup each: always from PUB_BIG_MAX leaves, and from
+    // PUB_BIG_MIN when the batch is too small to fill the GPU with one wave per document (for
+    // thousands of mid-sized documents one wave each moves more per second)
+    pub_small.clear();
+    pub_big.clear();
+    for (u64 d = 0; d < n_docs; d++) {
+      u32 nl = st_h[d].n_leaves;
+      bool big = nl >= PUB_BIG_MAX || (nl >= PUB_BIG_MIN && n_docs <= PUB_BIG_FEW_DOCS);
+      (big ? pub_big : pub_small).push_back((u32)d);
+    }
+    dfree(pub_list);
+    if (!pub_big.empty()) {
+      std::vector<u32> all(pub_small);
+      all.insert(all.end(), pub_big.begin(), pub_big.end());
+      HIPCHK(dalloc(pub_list, all.size()));
+      HIPCHK(hipMemcpyAsync(pub_list, all.data(), all.size() * 4, hipMemcpyHostToDevice, stream));
+    }
     HIPCHK(hipStreamSynchronize(stream));
     pub_sized = true;
     return 0;
@@ -727,9 +749,21 @@ struct crdt_engine {
       if (r) return r;
     }
     HIPCHK(hipEventRecord(ev[2], stream));
-    if (L == 32) hipLaunchKernelGGL(k_publish<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
-    else hipLaunchKernelGGL(k_publish<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
-    HIPCHK(hipGetLastError());
+    Pools pv = pools_view(pools);
+    PubOut ov = pub_view();
+    u32 ns = pub_list ? (u32)pub_small.size() : (u32)n_docs;
+    blocks = (ns + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    if (ns) {
+      if (L == 32) hipLaunchKernelGGL(k_publish<32>, dim3(blocks), dim3(256), 0, stream, pv, ov, ns, (const u32*)pub_list);
+      else hipLaunchKernelGGL(k_publish<4>, dim3(blocks), dim3(256), 0, stream, pv, ov, ns, (const u32*)pub_list);
+      HIPCHK(hipGetLastError());
+    }
+    if (pub_list && !pub_big.empty()) {
+      const u32* bl = pub_list + pub_small.size();
+      if (L == 32) hipLaunchKernelGGL(k_publish_big<32>, dim3((u32)pub_big.size()), dim3(64 * PUB_BIG_WAVES), 0, stream, pv, ov, bl);
+      else hipLaunchKernelGGL(k_publish_big<4>, dim3((u32)pub_big.size()), dim3(64 * PUB_BIG_WAVES), 0, stream, pv, ov, bl);
+      HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(ev[3], stream));
     published = true;
     materialized = false;

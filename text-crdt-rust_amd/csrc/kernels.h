@@ -186,33 +186,62 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
   return v;
 }
 
-template <int L>
-__global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
-  u32 d = uni(blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6));
-  if (d >= n) return;
-  __shared__ u32 s_flag[WAVES_PER_BLOCK][64];
-  WaveGPU<L> w;
-  DocState s = w.ldT(P.st + d);
-  DocSeg seg = w.ld_seg(P.seg + d);
-  u32 l = lane_id();
-  if ((s.status != ST_OK && s.status != ST_NEED_CAPACITY) || s.next_order >= seg.ord_cap) {
-    if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
-    return;
-  }
-  Span* canon = O.canon + seg.canon_base;
-  u32* vpos = O.vpos + seg.canon_base;
-  const u32 ccap = seg.canon_cap;  // (writes past it are dropped and reported below)
+// ---------------------------------------------------------------------------------------------
+// k_publish: the flat index of every document (canonical spans in document order, visible prefix,
+// order -> span index, digest).  One wave per document (k_publish), or for long documents one
+// workgroup of PUB_BIG_WAVES waves (k_publish_big): the leaf sequence is cut into one range per
+// wave, each wave compacts its range, the spans that cross range boundaries are resolved once,
+// and the index sweeps are split over the waves.
+// ---------------------------------------------------------------------------------------------
+#define PUB_BIG_WAVES 16
+#define PUB_BIG_MIN 2048u        // leaves from which a document may publish with a workgroup ...
+#define PUB_BIG_FEW_DOCS 1024u   // ... when the batch has at most this many documents
+#define PUB_BIG_MAX 16384u       // leaves from which it always does
+
+// What one wave's leaf range contributes (k_publish_big boundary resolution).
+struct RangeSum {
+  u32 spans;      // canonical spans starting in the range (its first entry counts as a start)
+  u32 vis;        // visible items
+  u32 single;     // the whole range is one span
+  i32 lead_len;   // signed length of the range's first span inside the range
+  Span first, last;  // first and last raw entries
+};
+
+// Canonical compaction of leaves [a, b) (directory order) by one wave, lane i = entry i of a leaf:
+// an entry starts a new span unless YjsSpan::can_append(previous entry, entry) (span.rs:47-53;
+// merging is transitive, so the previous raw entry stands for the open span); span lengths are
+// segmented sums of a prefix scan; the span still open at a leaf's end carries over (uniform
+// registers).  WRITE: spans go to canon/vpos from index `out` with visible offsets from `vis`;
+// skip_first: the range's first span continues the previous range's (not written); extra: the
+// signed length the range's last span continues by in later ranges.  !WRITE: fill `sum`.
+template <int L, bool WRITE>
+__device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg, u32 ng, u32 a, u32 b, Span* canon,
+                                              u32* vpos, u32 ccap, u32& out, u32& vis, u32 skip_first, i32 extra,
+                                              RangeSum& sum) {
+  const u32 l = lane_id();
   const Span* leaves = P.leaves + seg.leaf_base * L;
   const GroupRec* groups = P.groups + seg.grp_base;  // the root level, read in order from HBM
-  // Canonical spans, one leaf per step, lane i = entry i: an entry starts a new span unless
-  // YjsSpan::can_append(previous entry, entry) (span.rs:47-53; merging is transitive, so the
-  // previous raw entry stands for the open span); span lengths are segmented sums of a prefix
-  // scan; the span still open at the leaf's end carries over (uniform registers).
-  u32 out = 0, vis = 0, have = 0;
+  const u32 vis0 = vis;
+  u32 have = 0, skip = skip_first, nsp = 0, first_done = 0;
   Span open{0, 0, 0, 0};
   u32 open_vpos = 0;
-  for (u32 g = 0; g < s.ng; g++) {
+  // the group holding leaf a: prefix of the groups' slot counts
+  u32 g = 0, base = 0;
+  if (a) {
+    for (u32 r = 0; r < ng; r += 64) {
+      u32 c = r + l < ng ? groups[r + l].cnt : 0u;
+      u32 incl = wave_incl_scan(c);
+      u32 k = (u32)__popcll(ballot(r + l < ng && incl + base <= a));
+      if (k < 64u && r + k < ng) { g = r + k; base += k ? rdlane(incl, k - 1u) : 0u; break; }
+      base += rdlane(incl, 63);
+    }
+  }
+  for (u32 idx = a; g < ng && idx < b; g++) {
     u32 blk = uni(groups[g].blk), cnt = uni(groups[g].cnt);
+    u32 i0 = idx - base;        // first slot of this group in the range
+    base += cnt;
+    if (i0 >= cnt) continue;
+    u32 iend = b - (base - cnt) < cnt ? b - (base - cnt) : cnt;  // slot bound in this group
     u32 mydl = P.dir_leaf[(seg.blk_base + blk) * GROUP + l];  // 64-slot row: always in bounds
     // 64/L leaves per step: lane l holds entry l%L of leaf i + l/L; the valid entries (packed at
     // the front of each leaf) are then compacted to lanes [0, nn) with one ds_permute, so the
@@ -223,28 +252,29 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
     u32 sub = l / (u32)L;
     auto ld = [&](u32 i) -> uint4 {
       u32 li = i + sub;
-      u32 leaf = shfl(mydl, li < cnt ? li : 0u);
-      return li < cnt ? *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1))) : uint4{0, 0, 0, 0};
+      u32 leaf = shfl(mydl, li < iend ? li : 0u);
+      return li < iend ? *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1))) : uint4{0, 0, 0, 0};
     };
-    uint4 vn = cnt ? ld(0) : uint4{0, 0, 0, 0};
-    for (u32 i = 0; i < cnt; i += PER) {
+    uint4 vn = ld(i0);
+    for (u32 i = i0; i < iend; i += PER) {
       uint4 v = vn;
-      if (i + PER < cnt) vn = ld(i + PER);
+      if (i + PER < iend) vn = ld(i + PER);
       u64 VM = ballot(v.w != 0u);
       u32 nn = (u32)__popcll(VM);
       if (PER > 1) {
         u64 below = (1ull << l) - 1ull;
         u32 dst = v.w != 0u ? (u32)__popcll(VM & below) : nn + (u32)__popcll(~VM & below);
-        int a = (int)(dst << 2);
-        v.x = (u32)__builtin_amdgcn_ds_permute(a, (int)v.x);
-        v.y = (u32)__builtin_amdgcn_ds_permute(a, (int)v.y);
-        v.z = (u32)__builtin_amdgcn_ds_permute(a, (int)v.z);
-        v.w = (u32)__builtin_amdgcn_ds_permute(a, (int)v.w);
+        int ad = (int)(dst << 2);
+        v.x = (u32)__builtin_amdgcn_ds_permute(ad, (int)v.x);
+        v.y = (u32)__builtin_amdgcn_ds_permute(ad, (int)v.y);
+        v.z = (u32)__builtin_amdgcn_ds_permute(ad, (int)v.z);
+        v.w = (u32)__builtin_amdgcn_ds_permute(ad, (int)v.w);
       }
+      if (nn == 0u) continue;
       bool valid = l < nn;
       Span e{v.x, v.y, v.z, (i32)v.w};
       u32 px = shfl(v.x, l - 1u), py = shfl(v.y, l - 1u), pz = shfl(v.z, l - 1u), pw = shfl(v.w, l - 1u);
-      Span prev = l == 0u ? open : Span{px, py, pz, (i32)pw};
+      Span prev = l == 0u ? sum.last : Span{px, py, pz, (i32)pw};
       bool app = valid && (l != 0u || have) && can_append(prev, e);
       bool start = valid && !app;
       u64 M = ballot(start);
@@ -259,40 +289,68 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
       i32 glen = (i32)(p_end - (Pl - len_u));  // span starting at this lane: lanes [l, nxt)
       u32 fs = M ? (u32)__builtin_ctzll(M) : nn;
       if (have && fs) open.len += (i32)rdlane(Pl, fs - 1u);
+      if (!first_done) {
+        if (!have) sum.first = Span{rdlane(v.x, 0), rdlane(v.y, 0), rdlane(v.z, 0), (i32)rdlane(v.w, 0)};
+      }
       if (M) {
-        if (have) {
-          if (l == 0u && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
-          out++;
+        if (have) {  // the open span closes
+          if (!first_done) { sum.lead_len = open.len; first_done = 1; }
+          if (WRITE) {
+            if (skip) skip = 0;
+            else {
+              if (l == 0u && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
+              out++;
+            }
+          }
         }
         u32 ls = 63u - (u32)__builtin_clzll(M);
         u32 rank = (u32)__popcll(M & ((1ull << l) - 1ull));
-        if (start && l != ls && out + rank < ccap) {
-          canon[out + rank] = Span{v.x, v.y, v.z, glen};
-          vpos[out + rank] = vis + V - cl;
+        u32 firsts = (u32)__popcll(M) - 1u;  // spans that also close in this step
+        if (!first_done && firsts) { sum.lead_len = (i32)rdlane((u32)glen, fs); first_done = 1; }
+        if (WRITE) {
+          u32 sk = skip && firsts ? 1u : 0u;  // the skipped first span is the step's first start
+          if (start && l != ls && rank >= sk && out + rank - sk < ccap) {
+            canon[out + rank - sk] = Span{v.x, v.y, v.z, glen};
+            vpos[out + rank - sk] = vis + V - cl;
+          }
+          out += firsts - sk;
+          if (sk) skip = 0;
         }
-        out += (u32)__popcll(M) - 1u;
+        nsp += (u32)__popcll(M);
         open = Span{rdlane(v.x, ls), rdlane(v.y, ls), rdlane(v.z, ls), (i32)rdlane((u32)glen, ls)};
         open_vpos = vis + rdlane(V - cl, ls);
         have = 1;
       }
+      sum.last = Span{rdlane(v.x, nn - 1u), rdlane(v.y, nn - 1u), rdlane(v.z, nn - 1u), (i32)rdlane(v.w, nn - 1u)};
       vis += leaf_vis;
     }
+    idx = base;
   }
   if (have) {
-    if (l == 0 && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
-    out++;
+    if (!first_done) { sum.lead_len = open.len; sum.single = 1; }
+    else sum.single = 0;
+    if (WRITE && !skip) {
+      open.len += extra;
+      if (l == 0 && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
+      out++;
+    }
   }
-  if (out > ccap) {  // canonical spans beyond the planned capacity: report, never write past it
-    if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
-    return;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  // Order -> canonical span index (replaces a 4 B/order table): a bitmap over the
-  // orders with a bit at every canonical span's first order, the exclusive count of set bits
-  // before every word, and the spans listed by first order.  Built in three sweeps: set the bits
-  // (atomic OR: spans are in document order, not order order), prefix-count the words (wave
-  // scans), scatter every span to its rank.  Per document 2 bits per order + 4 B per span are
-  // written instead of 4 B per item order.  Reads go through L2 (ld_l2): other lanes wrote them.
+  sum.spans = nsp;
+  sum.vis = vis - vis0;
+}
+
+// Order -> canonical span index (replaces a 4 B/order table): a bitmap over the
+// orders with a bit at every canonical span's first order, the exclusive count of set bits before
+// every word, and the spans listed by first order.  Three sweeps: set the bits (atomic OR: spans
+// are in document order, not order order), prefix-count the words, scatter every span to its
+// rank.  Per document 2 bits per order + 4 B per span are written instead of 4 B per item order.
+// Reads go through L2 (ld_l2): other lanes wrote them.  Wave `wv` of `nwv` takes every nwv-th
+// chunk; the word prefix is one contiguous word range per wave plus a cross-wave carry (lds_c:
+// nwv u32 of LDS, k_publish_big only).  Returns this wave's share of the canonical-span hash.
+template <int NWV>
+__device__ __forceinline__ u64 publish_index(const PubOut& O, const DocSeg& seg, const DocState& s, const Span* canon,
+                                             u32 out, u32 wv, u32* lds_c) {
+  const u32 l = lane_id();
 #ifdef PUB_NO_INDEX
   const u32 nw = pub_words(seg.ord_cap), used = 0u;
 #else
@@ -301,10 +359,11 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   u32* bits = O.pub + seg.pub_base;
   u32* pre = bits + nw;
   u32* sorted = O.sorted + seg.canon_base;
-  for (u32 i = l; i < used; i += 64) bits[i] = 0u;
+  for (u32 i = wv * 64u + l; i < used; i += 64u * NWV) bits[i] = 0u;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (NWV > 1) __syncthreads();
   u64 h = 0;
-  for (u32 k0 = 0; k0 < out; k0 += 64) {
+  for (u32 k0 = wv * 64u; k0 < out; k0 += 64u * NWV) {
     u32 k = k0 + l;
     Span sp = k < out ? canon[k] : Span{0, 0, 0, 0};
     if (k < out) h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
@@ -322,25 +381,40 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
 #endif
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  // (4 steps per iteration: their loads are in flight together)
-  for (u32 i0 = 0, carry = 0; i0 < used; i0 += 256) {
+  // word prefix: this wave's contiguous word range [wa, wb), 4 steps per iteration (their loads
+  // in flight together)
+  const u32 per_wave = ((used + NWV - 1u) / NWV + 63u) & ~63u;
+  const u32 wa = wv * per_wave < used ? wv * per_wave : used, wb = wa + per_wave < used ? wa + per_wave : used;
+  u32 carry = 0;
+  if (NWV > 1) {
+    __syncthreads();  // every wave's atomics are done
+    u32 t = 0;
+    for (u32 i = wa + l; i < wb; i += 64) t += (u32)__popc(ld_l2(bits + i));
+    t = wave_sum(t);
+    if (l == 0) lds_c[wv] = t;
+    __syncthreads();
+    u32 c = l < wv ? lds_c[l] : 0u;
+    carry = wave_sum(c);
+  }
+  for (u32 i0 = wa; i0 < wb; i0 += 256) {
     u32 x[4];
 #pragma unroll
     for (u32 u = 0; u < 4; u++) {
       u32 i = i0 + 64 * u + l;
-      x[u] = i < used ? (u32)__popc(ld_l2(bits + i)) : 0u;
+      x[u] = i < wb ? (u32)__popc(ld_l2(bits + i)) : 0u;
     }
 #pragma unroll
     for (u32 u = 0; u < 4; u++) {
       u32 i = i0 + 64 * u + l;
       u32 incl = wave_incl_scan(x[u]);
-      if (i < used) pre[i] = carry + incl - x[u];
+      if (i < wb) pre[i] = carry + incl - x[u];
       carry += rdlane(incl, 63);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (NWV > 1) __syncthreads();
 #ifndef PUB_NO_INDEX
-  for (u32 k0 = 0; k0 < out; k0 += 256) {
+  for (u32 k0 = wv * 256u; k0 < out; k0 += 256u * NWV) {
     u32 o[4], r[4];
 #pragma unroll
     for (u32 u = 0; u < 4; u++) {
@@ -359,6 +433,15 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
     }
   }
 #endif
+  return h;
+}
+
+// The digest's other sections (client_with_order, deletes, double deletes, txns + parents,
+// frontier) by one wave, and the counts.  Identical to oracle/crdt_oracle.hpp digest().
+template <int L>
+__device__ __forceinline__ u64 digest_tables(const Pools& P, const DocSeg& seg, const DocState& s, WaveGPU<L>& w) {
+  const u32 l = lane_id();
+  u64 h = 0;
   const CwoRun* cwo = P.cwo + seg.cwo_base;
   for (u32 k = l; k < s.n_cwo; k += 64) {
     CwoRun r = cwo[k];
@@ -388,13 +471,112 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n) {
   }
   const u32* fr = P.frontier + seg.fr_base;
   for (u32 k = l; k < s.n_fr; k += 64) h += elem_hash(7, k, fr[k], 0);
-  h = wave_sum64(h);
+  return h;
+}
+__device__ __forceinline__ u64 digest_counts(const DocState& s, u32 out) {
   u64 counts = elem_hash(8, 0, ((u64)s.len << 32) | out, ((u64)s.n_cwo << 32) | s.n_del);
-  counts ^= elem_hash(9, 0, ((u64)s.n_dd << 32) | s.n_txn, ((u64)s.n_fr << 32) | s.n_par);
+  return counts ^ elem_hash(9, 0, ((u64)s.n_dd << 32) | s.n_txn, ((u64)s.n_fr << 32) | s.n_par);
+}
+
+template <int L>
+__global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n, const u32* list) {
+  u32 d;
+  if (!wave_doc(WAVES_PER_BLOCK, list, n, d)) return;
+  WaveGPU<L> w;
+  DocState s = w.ldT(P.st + d);
+  DocSeg seg = w.ld_seg(P.seg + d);
+  u32 l = lane_id();
+  if ((s.status != ST_OK && s.status != ST_NEED_CAPACITY) || s.next_order >= seg.ord_cap) {
+    if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
+    return;
+  }
+  Span* canon = O.canon + seg.canon_base;
+  u32* vpos = O.vpos + seg.canon_base;
+  u32 out = 0, vis = 0;
+  RangeSum sum{};
+  compact_range<L, true>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, seg.canon_cap, out, vis, 0u, 0, sum);
+  if (out > seg.canon_cap) {  // canonical spans beyond the planned capacity: report, never write past it
+    if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  u64 h = publish_index<1>(O, seg, s, canon, out, 0u, nullptr);
+  h += digest_tables<L>(P, seg, s, w);
+  h = wave_sum64(h);
   if (l == 0) {
     O.canon_n[d] = out;
     O.len[d] = s.len;
-    O.digest[d] = mix64(h ^ counts);
+    O.digest[d] = mix64(h ^ digest_counts(s, out));
+  }
+}
+
+// Long documents: one workgroup of PUB_BIG_WAVES waves per listed document.
+template <int L>
+__global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, PubOut O, const u32* list) {
+  constexpr u32 NWV = PUB_BIG_WAVES;
+  __shared__ RangeSum s_sum[NWV];
+  __shared__ u32 s_base[NWV], s_vbase[NWV], s_skip[NWV], s_c[NWV], s_total;
+  __shared__ i32 s_extra[NWV];
+  __shared__ u64 s_h[NWV];
+  const u32 d = list[blockIdx.x];
+  const u32 l = lane_id(), wv = uni(threadIdx.x >> 6);
+  WaveGPU<L> w;
+  DocState s = w.ldT(P.st + d);
+  DocSeg seg = w.ld_seg(P.seg + d);
+  if ((s.status != ST_OK && s.status != ST_NEED_CAPACITY) || s.next_order >= seg.ord_cap) {
+    if (threadIdx.x == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
+    return;
+  }
+  Span* canon = O.canon + seg.canon_base;
+  u32* vpos = O.vpos + seg.canon_base;
+  // this wave's leaves (every range holds leaves: the host sends only documents with many)
+  const u32 a = (u32)((u64)s.n_leaves * wv / NWV), b = (u32)((u64)s.n_leaves * (wv + 1u) / NWV);
+  u32 out = 0, vis = 0;
+  RangeSum sum{};
+  compact_range<L, false>(P, seg, s.ng, a, b, canon, vpos, seg.canon_cap, out, vis, 0u, 0, sum);
+  if (l == 0) s_sum[wv] = sum;
+  __syncthreads();
+  if (wv == 0) {  // boundary resolution, lane = range
+    RangeSum me = s_sum[l < NWV ? l : 0u];
+    Span prv = s_sum[l > 0u && l <= NWV ? l - 1u : 0u].last;
+    u32 merge = l > 0u && l < NWV && can_append(prv, me.first);
+    u32 cnt = l < NWV ? me.spans - merge : 0u;
+    u32 ci = wave_incl_scan(cnt), vi = wave_incl_scan(l < NWV ? me.vis : 0u);
+    if (l < NWV) { s_base[l] = ci - cnt; s_vbase[l] = vi - me.vis; s_skip[l] = merge; }
+    if (l == 0) s_total = rdlane(ci, NWV - 1u);
+    // extra_r = merge_{r+1} ? lead_{r+1} + (single_{r+1} ? extra_{r+1} : 0) : 0, from the last range back
+    i32 extra = 0;
+    for (i32 r = (i32)NWV - 1; r >= 0; r--) {
+      u32 mr = rdlane(merge, (u32)r + 1u < NWV ? (u32)r + 1u : 0u) & ((u32)r + 1u < NWV);
+      i32 nx = (i32)rdlane((u32)me.lead_len, (u32)r + 1u < NWV ? (u32)r + 1u : 0u);
+      u32 sg = rdlane(me.single, (u32)r + 1u < NWV ? (u32)r + 1u : 0u);
+      extra = mr ? nx + (sg ? extra : 0) : 0;
+      if (l == 0) s_extra[r] = extra;
+    }
+  }
+  __syncthreads();
+  out = s_base[wv];
+  vis = s_vbase[wv];
+  RangeSum sum2{};
+  compact_range<L, true>(P, seg, s.ng, a, b, canon, vpos, seg.canon_cap, out, vis, s_skip[wv], s_extra[wv], sum2);
+  const u32 total = s_total;
+  if (total > seg.canon_cap) {
+    if (threadIdx.x == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
+    return;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+  u64 h = publish_index<NWV>(O, seg, s, canon, total, wv, s_c);
+  if (wv == 0) h += digest_tables<L>(P, seg, s, w);
+  h = wave_sum64(h);
+  if (l == 0) s_h[wv] = h;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 t = 0;
+    for (u32 k = 0; k < NWV; k++) t += s_h[k];
+    O.canon_n[d] = total;
+    O.len[d] = s.len;
+    O.digest[d] = mix64(t ^ digest_counts(s, total));
   }
 }
 

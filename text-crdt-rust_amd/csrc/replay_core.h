@@ -607,7 +607,7 @@ struct Replayer {
 #endif
       u32 nl = split_at(c.idx, follow ? space : 0u);
 #ifdef CRDT_PROF
-      if (prof_mode == 3u) inc(S_PROF0, (u32)(w.clock() - ts));  // detail: split_at
+      (void)ts;
 #endif
       if (follow) {  // the cursor follows the new leaf; its first `space` slots are padding
         u32 nblk = g(C_BLK), ni = g(C_I) + 1u;  // nl sits right after the old leaf
@@ -966,6 +966,9 @@ struct Replayer {
   // inl: the txn's single op (and for a remote txn its single parent) are gop / gpar, not records
   // after the header (a compact record, or a generated op)
   CRDT_HD i32 apply_txn(const Rec& h, u32 pos, bool remote, u32 inl, const Rec& gop, const Rec& gpar) {
+#ifdef CRDT_PROF
+    u64 prof_t0 = w.clock();
+#endif
     u32 nops, agent, np = 0, seq, txn_len;
     if (!remote) {
       nops = h.w0 & 0x0FFFFFFFu;
@@ -1167,7 +1170,14 @@ struct Replayer {
         else w.st(pp + j, o);  // pp[0] is written by insert_txn (only if the txn is kept)
       }
     }
+#ifdef CRDT_PROF
+    u64 prof_t1 = w.clock();
+    i32 rst = insert_txn(remote, first, txn_len, np, p0);
+    (void)prof_t0;
+    return rst;
+#else
     return insert_txn(remote, first, txn_len, np, p0);
+#endif
   }
 
   // ------------------------------------------------------------------ fast paths
@@ -1387,9 +1397,15 @@ struct Replayer {
           if (n2 <= 1u) break;
           k += n2 - 1u;
         }
+#ifdef CRDT_PROF
+        if (prof_mode == 3u && k > room) inc(S_PROF0);  // detail: run cut by the entry / item_orders room
+#endif
         k = k < room ? k : room;
       }
     }
+#ifdef CRDT_PROF
+    if (prof_mode == 3u) { inc(S_PROF3); if (k == 1u) inc(S_PROF2); }  // detail: delete calls, single deletes
+#endif
     if ((g(K_MAP) - first < k * l) | (g(K_DEL) - g(S_N_DEL) < k)) return 0;
     u32 done = k >= 2u ? delete_run_closed(idx, off, t1, k, back) : 0u;
     if (done == 0u) {  // op by op
@@ -1403,6 +1419,9 @@ struct Replayer {
       }
     }
     if (done == 0u) return 0;
+#ifdef CRDT_PROF
+    if (prof_mode == 3u && done < k) inc(S_PROF1);  // detail: run cut by the leaf (closed form / op by op)
+#endif
     if (back) {  // doc.rs:305-308 / 420-423: backspaced targets never coalesce: one run each
       append_delete(first, t1, 1u);
       if (done > 1u) {
@@ -1606,9 +1625,7 @@ struct Replayer {
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
         u32 dt = prof_mode == 0u ? (u32)(t1 - t0) : prof_mode == 1u ? 1u : (fast ? fast / per_txn(kind == REC_RTXN || kind == REC_RC) : 0u);
-        if (prof_mode == 3u) {  // detail: fast ok / failed attempt
-          if (fast) inc(S_PROF3, (u32)(t1 - t0));
-          else inc(S_PROF2, (u32)(t1 - t0));
+        if (prof_mode == 3u) {  // detail: apply_txn parts (below)
         } else if (!fast) inc(S_PROF1, prof_mode == 0u ? dt : 0u);
         else if (prof_cat == 0u) inc(S_PROF0, dt);
         else if (prof_cat == 2u) inc(S_PROF2, dt);
@@ -1627,7 +1644,7 @@ struct Replayer {
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, inl, gop, gpar) : ST_BAD_INPUT;
         pre = 0;
 #ifdef CRDT_PROF
-        inc(S_PROF1, (prof_mode == 0u || prof_mode == 3u) ? (u32)(w.clock() - t1) : 1u);  // detail: apply_txn
+        if (prof_mode != 3u) inc(S_PROF1, prof_mode == 0u ? (u32)(w.clock() - t1) : 1u);
 #endif
       } else if (kind == REC_PROBE) {
         probe(h, pos);
