@@ -27,6 +27,9 @@ else:
     e.stage_remote_replicated(w, 0, ["u%05d" % i for i in range(a.docs)])
 t0 = time.time()
 st = e.run()
+e.publish_async()
+e.sync()
+e.fit()  # as bench.py: capacities = the stream's use
 if a.clean:
     e.reset_async()
     e.run_async()
