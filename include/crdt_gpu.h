@@ -183,7 +183,6 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
                 uint32_t* cwo4, uint32_t* del3, uint32_t* dd3, uint32_t* txn5, uint32_t* parents,
                 uint32_t* frontier);
 
-/* Raw per-document replay state (22 u32: status, resume point, table sizes, ...; debugging). */
 // Shrink every document's per-table capacities to what its staged stream used (call after a
 // crdt_run + publish of it; a later reset + crdt_run_async replays it in exactly that room).
 // Capacities grow again on the next stage.  (Host-side planning; no reference counterpart.)
@@ -203,6 +202,7 @@ typedef struct { uint32_t agent, seq, pos, deleted; } crdt_probe_answer;
 int crdt_apply_local_probed(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
                             const crdt_local_txn* txns, const crdt_local_op* ops, const crdt_probe* probes,
                             crdt_probe_answer* answers, int32_t* doc_status);
+/* Raw per-document replay state (23 u32: status, resume point, table sizes, ...; debugging). */
 int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23);
 /* Device time of the last replay / publish launches in ms (HIP events on the engine stream). */
 int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms);
