@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--docs", type=int, default=64)
 ap.add_argument("--trace", default="automerge-paper")
 ap.add_argument("--local", action="store_true")
+ap.add_argument("--wire", default=None, help="a .rtx.gz remote wire file instead of a trace")
 ap.add_argument("--clean", action="store_true", help="reset and replay once more (single launch)")
 a = ap.parse_args()
 e = crdt_amd.Engine(a.docs, 32)
@@ -23,7 +24,11 @@ if a.local:
     ag = e.agent_intern(list(range(a.docs)), ["jeremy"] * a.docs)
     e.apply_trace(list(range(a.docs)), int(ag[0]), t.counts, t.patches, stage_only=True)
 else:
-    w = load_remote_wire(a.trace)
+    if a.wire:
+        import gzip
+        w = gzip.open(a.wire, "rb").read()
+    else:
+        w = load_remote_wire(a.trace)
     e.stage_remote_replicated(w, 0, ["u%05d" % i for i in range(a.docs)])
 t0 = time.time()
 st = e.run()

@@ -70,7 +70,9 @@ enum : u32 {
   T_RB_BASE,
   P_DDB,  // (2 slots) double-delete block directory
   P_PROBE = P_DDB + 2,  // (2 slots) probe answers
-  N_SLOTS = P_PROBE + 2
+  // 1: the txn-level invariants fast_txn_ok checks hold (set by a fast commit, cleared by apply_txn)
+  F_FAST = P_PROBE + 2,
+  N_SLOTS
 };
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
 static_assert(S_PROF3 < K_FR, "DocState lives in the first context register");
@@ -189,6 +191,7 @@ struct Replayer {
     p(T_AG_ID, INVALID); p(T_AG_BASE, 0); p(T_AG_CNT, 0); p(T_AG_CAP, 0);
     p(T_AGL_KEY, 0); p(T_AGL_ORDER, 0); p(T_AGL_LEN, 0);
     p(T_RB_BASE, 0x80000000u);  // pos - rb_base >= 64 for every valid pos
+    p(F_FAST, 0);
   }
 
   CRDT_HD Span* leafp(u32 leaf) const { return lv() + (u64)leaf * L; }
@@ -969,6 +972,7 @@ struct Replayer {
 #ifdef CRDT_PROF
     u64 prof_t0 = w.clock();
 #endif
+    p(F_FAST, 0u);  // the general path changes the tails fast_txn_ok relies on
     u32 nops, agent, np = 0, seq, txn_len;
     if (!remote) {
       nops = h.w0 & 0x0FFFFFFFu;
@@ -1193,8 +1197,14 @@ struct Replayer {
   // continues its agent's last item_orders run and the last client_with_order run, its single
   // parent is the previous order, the frontier is that one order, so the txn coalesces into the
   // last TxnSpan (TxnSpan::can_append, txn.rs:44-48: shadow unchanged, parents not kept).
+  //
+  // A fast commit (fast_txn_commit) extends every one of these tails by the txn, so after it all
+  // conditions that do not name the next txn's author and seq still hold (F_FAST); only
+  // apply_txn changes them otherwise.  Then the check is: same author, next seq.
   CRDT_HD u32 fast_txn_ok(u32 agent, u32 seq, u32 first) const {
-    u32 ll = g(T_AGL_LEN), cl = g(T_CWO_LEN);
+    u32 ll = g(T_AGL_LEN);
+    if (g(F_FAST)) return (agent == g(T_AG_ID)) & (seq == g(T_AGL_KEY) + ll);
+    u32 cl = g(T_CWO_LEN);
     return (agent == g(T_AG_ID)) & (g(T_AG_CNT) != 0u) & (seq == g(T_AGL_KEY) + ll) &
            (g(T_AGL_ORDER) + ll == first) & (g(S_N_CWO) != 0u) & (g(T_CWO_AGENT) == agent) &
            (g(T_CWO_SEQ) + cl == seq) & (g(T_CWO_KEY) + cl == first) & (g(S_N_FR) == 1u) &
@@ -1207,6 +1217,7 @@ struct Replayer {
     p(T_FR0, first + len - 1u);
     inc(T_TX_LEN, len);
     p(S_CAP_NEED, 0u);
+    p(F_FAST, 1u);
   }
   // the first order after entry idx of the cached leaf (get_item at the entry's end, cursor.rs:233-239)
   CRDT_HD u32 next_item_after(u32 idx, u32& order) {
@@ -1478,23 +1489,27 @@ struct Replayer {
     u32 b0 = 0, nv = 0;
     Rec h = gh, o = go, pr{0, 0, 0, 0};
     if (!gen) {
-      if (rn - pos < per) return 0;
+      // run() read the record at pos through the window (gh): a compact txn is that one record
       b0 = pos - g(T_RB_BASE);
-      if (b0 + per > 64u) {  // move the window to the txn (and what follows it)
-        rec_window(pos);
-        b0 = 0;
-      }
-      nv = rn - g(T_RB_BASE);
-      nv = nv < 64u ? nv : 64u;
-      h = w.rec_get(b0);
       if (cpt) {
         if (remote) expand_rc(h, h, o, pr);
         else expand_lc(h, h, o);
       } else {
+        if (rn - pos < per) return 0;
+        if (b0 + per > 64u) {  // move the window to the txn (and what follows it)
+          rec_window(pos);
+          b0 = 0;
+        }
+        h = w.rec_get(b0);
         o = w.rec_get(b0 + 1u);
         if (remote) pr = w.rec_get(b0 + 2u);
       }
+      nv = rn - g(T_RB_BASE);
+      nv = nv < 64u ? nv : 64u;
     }
+    // compact records and generated ops are one-op txns by construction (expand_rc / expand_lc
+    // / gen_op): only the general form needs its header checked
+    u32 gen_form = !(cpt | gen);
     u32 first = g(S_NEXT_ORDER);
     u32 agent, l, ins, ol = 0, orr = ROOT_ORDER;
     Cursor c;
@@ -1504,9 +1519,14 @@ struct Replayer {
       l = o.w0 & 0x0FFFFFFFu;
       u32 k = rec_kind(o);
       ins = k == REC_RINS;
-      u32 ok = (h.w0 == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
-               (pr.w0 == (REC_RPARENT << 28)) & (pr.w1 == agent) & (pr.w2 == seq - 1u) & (ins | (k == REC_RDEL));
-      if (!ok || !fast_txn_ok(agent, seq, first)) return 0;
+      if (gen_form) {
+        u32 ok = (h.w0 == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
+                 (pr.w0 == (REC_RPARENT << 28)) & (pr.w1 == agent) & (pr.w2 == seq - 1u) & (ins | (k == REC_RDEL));
+        if (!ok) return 0;
+      } else if (l == 0u) {
+        return 0;
+      }
+      if (!fast_txn_ok(agent, seq, first)) return 0;
       if (id_to_order(o.w1 & 0xFFFFu, o.w2, ol) != ST_OK || ol == ROOT_ORDER) return 0;  // origin_left / target
       if (ins && id_to_order(o.w1 >> 16, o.w3, orr) != ST_OK) return 0;
       if (!find_order(ol, true, c)) return 0;  // doc.rs:101-136 (loads the item's leaf)
@@ -1516,8 +1536,8 @@ struct Replayer {
       u32 lp = o.w1, del = o.w2;
       ins = o.w3 != 0u;
       l = del + o.w3;
-      u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l) &
-               ((del != 0u) != ins) & (l - 1u < 0xFFFFu) & ((lp != 0u) | !ins);
+      u32 ok = ((del != 0u) != ins) & (l - 1u < 0xFFFFu) & ((lp != 0u) | !ins);
+      if (gen_form) ok &= (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l);
       if (!ok || !fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first)) return 0;
       if (!cursor_at_content_pos(ins ? lp - 1u : lp, c)) return 0;  // root.rs:54-88 (loads the leaf)
       ol = w.cget_order(c.idx) + c.off;  // doc.rs:446-449: the item at pos - 1, then Cursor::next

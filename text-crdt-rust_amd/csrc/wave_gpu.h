@@ -14,7 +14,8 @@ namespace crdt {
 __device__ __forceinline__ u32 lane_id() { return __lane_id(); }
 __device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ u32 rdlane(u32 x, u32 l) { return __builtin_amdgcn_readlane(x, l); }
-__device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
+// (the builtin takes the i1 predicate directly: no v_cndmask + v_cmp round trip as __ballot has)
+__device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ u32 shfl(u32 v, u32 src) { return __builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
 
 // Inclusive wave64 prefix sum (LLVM AMDGPUAtomicOptimizer GFX9 sequence).
