@@ -150,7 +150,25 @@ struct WaveCPU {
     for (u32 i = 0; i < n_ahead; i++) qb[i] = p_ahead[i];
   }
   Rec rec_get(u32 k) const { return rb[k]; }
+  // the GPU backend's scans over 64 records at p (no window move); len0 = the first txn's length
+  u32 typing_scan_at(const Rec* p, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3, u32& total, u32& len0) const {
+    Rec t[64];
+    for (u32 i = 0; i < nv; i++) t[i] = p[i];
+    len0 = (compact & remote) ? rc_len(t[0]) : t[0].w3;
+    return typing_scan_b(t, 0u, nv, remote, compact, agent, ow1, ow3, total);
+  }
+  u32 delete_scan_at(const Rec* p, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+    Rec t[64];
+    for (u32 i = 0; i < nv; i++) t[i] = p[i];
+    return delete_scan_b(t, 0u, nv, remote, compact, agent, delta);
+  }
   u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3, u32& total) const {
+    return typing_scan_b(rb, b0, nv, remote, compact, agent, ow1, ow3, total);
+  }
+  u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+    return delete_scan_b(rb, b0, nv, remote, compact, agent, delta);
+  }
+  static u32 typing_scan_b(const Rec* rb, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3, u32& total) {
     if (compact) {
       u32 n = 1;
       total = remote ? rc_len(rb[b0]) : rb[b0].w3;
@@ -196,7 +214,7 @@ struct WaveCPU {
     return n;
   }
 
-  u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+  static u32 delete_scan_b(const Rec* rb, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) {
     if (compact) {
       u32 n = 1;
       for (u32 j = b0 + 1; j < nv; j++) {

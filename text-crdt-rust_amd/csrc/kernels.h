@@ -78,8 +78,13 @@ __global__ __launch_bounds__(256) void k_init(Pools P, u32 n, u32 wpb, u32 rcap)
 }
 
 // n: waves of this launch (documents in `list`, or the first n documents)
+// Register budget: 8 waves per SIMD (<= 64 VGPRs, <= 80 SGPRs).  Each document is one dependent
+// chain, so resident waves are what hides its latencies: 8 waves/SIMD replays 8,192 automerge-paper
+// documents in 185 ms where the compiler's own choice (84 VGPRs: 5 waves/SIMD) takes 199 ms and
+// 97 VGPRs (4 waves/SIMD) took 216 ms (scripts/gpu_ab.sh).  What the budget costs is a few spills
+// in cold paths.
 template <int L>
-__global__ __launch_bounds__(256) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
   u32 d;
   if (!wave_doc(wpb, list, n, d)) return;
   Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(rcap));

@@ -99,11 +99,6 @@ struct Replayer {
     else expand_lc(r, h, o);
     return o;
   }
-  // the length of the one-op txn at window slot b
-  CRDT_HD u32 len_at(u32 b, u32 remote) const {
-    Rec r = w.rec_get(b);
-    return (cpt & remote) ? rc_len(r) : r.w3;  // (a typing / delete-run LC has del = 0 or ins = 0)
-  }
 #ifdef CRDT_PROF
   u32 prof_cat = 0;  // diagnostic: which fast path ran (0 typing, 2 delete, 3 insert)
   u32 prof_mode = 0; // document d % 4: 0 cycles, 1 calls, 2 txns per path, 3 detail (below)
@@ -276,10 +271,19 @@ struct Replayer {
     else w.rec_load2(recs() + base, nn < 64u ? nn : 64u, ahead < 64u ? ahead : 64u);
     p(T_RB_BASE, base);
   }
+  // The record at pos, moving the window so that it holds [pos, pos + 3) (a whole general-form
+  // one-op txn).  The ONLY place the window moves: its registers then have one definition in the
+  // replay loop, so the compiler keeps them in place instead of copying them at every merge.
   CRDT_HD Rec rec(u32 pos) {
-    u32 d = pos - g(T_RB_BASE);
-    if (d >= 64u) rec_window(d < 128u ? g(T_RB_BASE) + 64u : pos);
+    u32 base = g(T_RB_BASE);
+    u32 d = pos - base;
+    if (d > 61u) rec_window(d <= 64u ? pos : (d < 125u ? base + 64u : pos));
     return w.rec_get(pos - g(T_RB_BASE));
+  }
+  // The record at pos without moving the window (general path: from HBM when outside it).
+  CRDT_HD Rec rec_at(u32 pos) const {
+    u32 d = pos - g(T_RB_BASE);
+    return d < 64u ? w.rec_get(d) : w.ld_rec(recs() + pos);
   }
 
   // ------------------------------------------------------------------ directory
@@ -1015,7 +1019,7 @@ struct Replayer {
       // ---------------------------------------------------------------- next op
       if (mode == M_FETCH) {
         if (k == nops) break;
-        Rec op = inl ? gop : rec(pos + 1 + k);
+        Rec op = inl ? gop : rec_at(pos + 1 + k);
         k++;
         if (!remote) {  // LocalOp: delete (visible range) first, then insert (doc.rs:386-465)
           lpos = op.w1;
@@ -1165,7 +1169,7 @@ struct Replayer {
     if (remote) {
       u32* pp = par() + g(S_N_PAR);
       for (u32 j = 0; j < np; j++) {
-        Rec pr = inl ? gpar : rec(pos + 1 + nops + j);
+        Rec pr = inl ? gpar : rec_at(pos + 1 + nops + j);
         if (rec_kind(pr) != REC_RPARENT) return ST_BAD_INPUT;
         u32 o;
         i32 st = id_to_order(pr.w1 & 0xFFFFu, pr.w2, o);
@@ -1242,14 +1246,15 @@ struct Replayer {
     nt = w.typing_scan(b0, nv, remote, cpt, agent, ow1, o.w3, total);
     u32 per = per_txn(remote), rn = rec_n();
     u32 pos0 = g(T_RB_BASE) + b0;
-    while ((pos0 + (nt + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
+    u32 end = g(T_RB_BASE) + nv;  // records scanned so far: [pos0, end)
+    while ((pos0 + (nt + 1u) * per > end) & (end < rn)) {  // the run reaches the end: scan on
       u32 last = pos0 + (nt - 1u) * per;
-      rec_window(last);
-      nv = rn - last < 64u ? rn - last : 64u;
-      u32 t2;
-      u32 n2 = w.typing_scan(0u, nv, remote, cpt, agent, ow1, o.w3, t2);
+      u32 n = rn - last < 64u ? rn - last : 64u;
+      u32 t2, l0;
+      u32 n2 = w.typing_scan_at(recs() + last, n, remote, cpt, agent, ow1, o.w3, t2, l0);
+      end = last + n;
       if (n2 <= 1u) break;
-      total += t2 - len_at(0u, remote);
+      total += t2 - l0;
       nt += n2 - 1u;
     }
     return nt;
@@ -1400,11 +1405,12 @@ struct Replayer {
         // the run may go on past the window: slide the window to its last txn and scan on
         u32 rn = rec_n();
         u32 pos0 = g(T_RB_BASE) + b0;
-        while ((k < room) & (pos0 + (k + 1u) * per > g(T_RB_BASE) + nv) & (g(T_RB_BASE) + nv < rn)) {
+        u32 end = g(T_RB_BASE) + nv;
+        while ((k < room) & (pos0 + (k + 1u) * per > end) & (end < rn)) {
           u32 last = pos0 + (k - 1u) * per;
-          rec_window(last);
-          nv = rn - last < 64u ? rn - last : 64u;
-          u32 n2 = w.delete_scan(0u, nv, remote, cpt, agent, delta);
+          u32 n = rn - last < 64u ? rn - last : 64u;
+          u32 n2 = w.delete_scan_at(recs() + last, n, remote, cpt, agent, delta);
+          end = last + n;
           if (n2 <= 1u) break;
           k += n2 - 1u;
         }
@@ -1495,11 +1501,7 @@ struct Replayer {
         if (remote) expand_rc(h, h, o, pr);
         else expand_lc(h, h, o);
       } else {
-        if (rn - pos < per) return 0;
-        if (b0 + per > 64u) {  // move the window to the txn (and what follows it)
-          rec_window(pos);
-          b0 = 0;
-        }
+        if (rn - pos < per) return 0;  // (rec() left the whole txn inside the window: b0 <= 61)
         h = w.rec_get(b0);
         o = w.rec_get(b0 + 1u);
         if (remote) pr = w.rec_get(b0 + 2u);

@@ -405,21 +405,21 @@ struct WaveGPU {
   // The txn at b0 was checked by the caller.  Returns the run length in txns (>= 1) and the
   // total inserted length.  nv = valid records in the block.
   // compact: one record per txn (crdt_types.h RC / LC), lane k checks record k against record k-1.
-  __device__ __forceinline__ u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3,
-                                             u32& total) const {
+  __device__ __forceinline__ static u32 typing_scan_r(u32 X, u32 Y, u32 Z, u32 Q, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3,
+                                             u32& total) {
     u32 l = lane_id();
     if (compact) {
-      u32 p0 = shfl(rx, l - 1u), p1 = shfl(ry, l - 1u), p3 = shfl(rw, l - 1u);
+      u32 p0 = shfl(X, l - 1u), p1 = shfl(Y, l - 1u), p3 = shfl(Q, l - 1u);
       bool ok;
       u32 hl;
       if (remote) {
-        hl = (rx >> 16) & 0x7FFu;
-        u32 ra = rw == 0xFFFFFFFFu ? 0xFFFFu : agent;  // origin_right's agent (ROOT or the author)
-        ok = (rx & RC_HDR_MASK) == ((REC_RC << 28) | agent) && hl != 0u && ry == p1 + ((p0 >> 16) & 0x7FFu) &&
-             rz == ry - 1u && rw == ow3 && (agent | (ra << 16)) == ow1;
+        hl = (X >> 16) & 0x7FFu;
+        u32 ra = Q == 0xFFFFFFFFu ? 0xFFFFu : agent;  // origin_right's agent (ROOT or the author)
+        ok = (X & RC_HDR_MASK) == ((REC_RC << 28) | agent) && hl != 0u && Y == p1 + ((p0 >> 16) & 0x7FFu) &&
+             Z == Y - 1u && Q == ow3 && (agent | (ra << 16)) == ow1;
       } else {
-        hl = rw;
-        ok = rx == ((REC_LC << 28) | agent) && rz == 0u && rw - 1u < 0xFFFFu && ry == p1 + p3;
+        hl = Q;
+        ok = X == ((REC_LC << 28) | agent) && Z == 0u && Q - 1u < 0xFFFFu && Y == p1 + p3;
       }
       u64 stop = ballot(l > b0 && (!ok || l >= nv));
       u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
@@ -433,21 +433,21 @@ struct WaveGPU {
     bool ok;
     if (remote) {
       u32 src = r == 0u ? l - 3u : (r == 1u ? l - 1u : l - 2u);  // previous header / own header
-      u32 hs = shfl(rz, src), hl = shfl(rw, src);
-      bool okh = rx == ((REC_RTXN << 28) | 1u) && ry == (agent | (1u << 16)) && rz == hs + hl && rw - 1u < 0xFFFFu;
-      bool oko = (rx >> 28) == REC_RINS && (rx & 0x0FFFFFFFu) == hl && ry == ow1 && rw == ow3 && rz == hs - 1u;
-      bool okp = rx == (REC_RPARENT << 28) && ry == agent && rz == hs - 1u;
+      u32 hs = shfl(Z, src), hl = shfl(Q, src);
+      bool okh = X == ((REC_RTXN << 28) | 1u) && Y == (agent | (1u << 16)) && Z == hs + hl && Q - 1u < 0xFFFFu;
+      bool oko = (X >> 28) == REC_RINS && (X & 0x0FFFFFFFu) == hl && Y == ow1 && Q == ow3 && Z == hs - 1u;
+      bool okp = X == (REC_RPARENT << 28) && Y == agent && Z == hs - 1u;
       ok = r == 0u ? okh : (r == 1u ? oko : okp);
     } else {
-      u32 hl = shfl(rw, l - 1u), ps = shfl(ry, l - 2u), pl = shfl(rw, l - 2u);
-      bool okh = rx == ((REC_LTXN << 28) | 1u) && ry == agent && rz == 0u && rw - 1u < 0xFFFFu;
-      bool oko = rx == (REC_LOP << 28) && rz == 0u && rw == hl && ry == ps + pl;
+      u32 hl = shfl(Q, l - 1u), ps = shfl(Y, l - 2u), pl = shfl(Q, l - 2u);
+      bool okh = X == ((REC_LTXN << 28) | 1u) && Y == agent && Z == 0u && Q - 1u < 0xFFFFu;
+      bool oko = X == (REC_LOP << 28) && Z == 0u && Q == hl && Y == ps + pl;
       ok = r == 0u ? okh : oko;
     }
     u64 stop = ballot(l >= b0 + per && (!ok || l >= nv));
     u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
     u32 n = remote ? ((f - b0) * 43u) >> 7 : (f - b0) >> 1;
-    total = wave_sum(l >= b0 && r == 0u && t < n ? rw : 0u);
+    total = wave_sum(l >= b0 && r == 0u && t < n ? Q : 0u);
     return n;
   }
 
@@ -456,12 +456,12 @@ struct WaveGPU {
   // seq + 1, RDEL of 1 item of `agent` at the previous target seq + delta, RPARENT (agent, seq-1);
   // local: LTXN{1 op} deleting 1 item at the previous pos + delta.  Returns the run length in
   // txns (>= 1; the txn at b0 was checked by the caller).
-  __device__ __forceinline__ u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+  __device__ __forceinline__ static u32 delete_scan_r(u32 X, u32 Y, u32 Z, u32 Q, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) {
     u32 l = lane_id();
     if (compact) {  // one record per txn: lane k against record k-1
-      u32 p1 = shfl(ry, l - 1u), p2 = shfl(rz, l - 1u);
-      bool ok = remote ? ((rx == ((REC_RC << 28) | (1u << 27) | (1u << 16) | agent)) && ry == p1 + 1u && rz == p2 + delta)
-                       : (rx == ((REC_LC << 28) | agent) && rz == 1u && rw == 0u && ry == p1 + delta);
+      u32 p1 = shfl(Y, l - 1u), p2 = shfl(Z, l - 1u);
+      bool ok = remote ? ((X == ((REC_RC << 28) | (1u << 27) | (1u << 16) | agent)) && Y == p1 + 1u && Z == p2 + delta)
+                       : (X == ((REC_LC << 28) | agent) && Z == 1u && Q == 0u && Y == p1 + delta);
       u64 stop = ballot(l > b0 && (!ok || l >= nv));
       u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
       return f - b0;
@@ -472,20 +472,39 @@ struct WaveGPU {
     u32 r = rel - t * per;
     bool ok;
     if (remote) {
-      u32 ps = shfl(rz, r == 2u ? l - 2u : l - 3u);  // previous header / previous op / own header
-      bool okh = rx == ((REC_RTXN << 28) | 1u) && ry == (agent | (1u << 16)) && rz == ps + 1u && rw == 1u;
-      bool oko = rx == ((REC_RDEL << 28) | 1u) && ry == agent && rz == ps + delta;
-      bool okp = rx == (REC_RPARENT << 28) && ry == agent && rz == ps - 1u;
+      u32 ps = shfl(Z, r == 2u ? l - 2u : l - 3u);  // previous header / previous op / own header
+      bool okh = X == ((REC_RTXN << 28) | 1u) && Y == (agent | (1u << 16)) && Z == ps + 1u && Q == 1u;
+      bool oko = X == ((REC_RDEL << 28) | 1u) && Y == agent && Z == ps + delta;
+      bool okp = X == (REC_RPARENT << 28) && Y == agent && Z == ps - 1u;
       ok = r == 0u ? okh : (r == 1u ? oko : okp);
     } else {
-      u32 pp = shfl(ry, l - 2u);  // previous op's pos
-      bool okh = rx == ((REC_LTXN << 28) | 1u) && ry == agent && rz == 1u && rw == 1u;
-      bool oko = rx == (REC_LOP << 28) && rz == 1u && rw == 0u && ry == pp + delta;
+      u32 pp = shfl(Y, l - 2u);  // previous op's pos
+      bool okh = X == ((REC_LTXN << 28) | 1u) && Y == agent && Z == 1u && Q == 1u;
+      bool oko = X == (REC_LOP << 28) && Z == 1u && Q == 0u && Y == pp + delta;
       ok = r == 0u ? okh : oko;
     }
     u64 stop = ballot(l >= b0 + per && (!ok || l >= nv));
     u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
     return remote ? ((f - b0) * 43u) >> 7 : (f - b0) >> 1;
+  }
+  // The scans over the record window, and over the 64 records at p (loaded here, waited for; the
+  // window does not move: only Replayer::rec moves it).  len0: the length of the txn at p.
+  __device__ __forceinline__ u32 typing_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3,
+                                             u32& total) const {
+    return typing_scan_r(rx, ry, rz, rw, b0, nv, remote, compact, agent, ow1, ow3, total);
+  }
+  __device__ __forceinline__ u32 typing_scan_at(const Rec* p, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1,
+                                                u32 ow3, u32& total, u32& len0) const {
+    uint4 v = rec_lane_load(p, nv);
+    len0 = (compact & remote) ? (rdlane(v.x, 0) >> 16) & 0x7FFu : rdlane(v.w, 0);
+    return typing_scan_r(v.x, v.y, v.z, v.w, 0u, nv, remote, compact, agent, ow1, ow3, total);
+  }
+  __device__ __forceinline__ u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+    return delete_scan_r(rx, ry, rz, rw, b0, nv, remote, compact, agent, delta);
+  }
+  __device__ __forceinline__ u32 delete_scan_at(const Rec* p, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+    uint4 v = rec_lane_load(p, nv);
+    return delete_scan_r(v.x, v.y, v.z, v.w, 0u, nv, remote, compact, agent, delta);
   }
   // runs {key0 + j, t0 - j, 1} for j < cnt (backspaced deletes), lane-parallel
   __device__ __forceinline__ void st_del_run(DelRun* p, u32 cnt, u32 key0, u32 t0) const {
