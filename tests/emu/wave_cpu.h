@@ -44,6 +44,7 @@ struct WaveCPU {
   TxnRec ld_txn(const TxnRec* p) const { return *p; }
   void st_txn(TxnRec* p, const TxnRec& v) const { *p = v; }
   Rec ld_rec(const Rec* p) const { return *p; }
+  template <u32 M = 1, class T> static T* at(T* base, u32 idx) { return base + (u64)idx * M; }
   void st_state(DocState* p, const DocState& s) const { *p = s; }
   DocState ld_state(const DocState* p) const { return *p; }
   DocSeg ld_seg(const DocSeg* p) const { return *p; }

@@ -77,8 +77,28 @@ CRDT_HD Span truncate_keeping_right(Span& s, u32 at) {  // span.rs:68-85
   s.len -= at_s;
   return o;
 }
+// An opaque copy of a wave-uniform integer: the compiler cannot see it is a 0/1 compare result,
+// so it stays a u32 in an SGPR (one s_cmp to branch on) instead of a 64-bit lane mask that every
+// later use re-combines with exec.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ u32 opq(u32 x) {
+  x = __builtin_amdgcn_readfirstlane(x);  // (free for a value already in an SGPR)
+  asm("" : "+s"(x));
+  return x;
+}
+#else
+inline u32 opq(u32 x) { return x; }
+#endif
 CRDT_HD bool can_append(const Span& a, const Span& b) {  // span.rs:47-53
   return ((a.len > 0) == (b.len > 0)) && b.order == a.order + slen(a) && b.ol == b.order - 1 && b.orr == a.orr;
+}
+// The same test as early exits, for wave-uniform operands (the replay's scalar code): a branch per
+// condition instead of lane-mask booleans.  (can_append stays branch-free for lane-parallel use.)
+CRDT_HD bool can_append_u(const Span& a, const Span& b) {
+  if ((a.len > 0) != (b.len > 0)) return false;
+  if (b.order != a.order + slen(a)) return false;
+  if (b.ol != b.order - 1) return false;
+  return b.orr == a.orr;
 }
 
 struct CwoRun { u32 key, agent, seq, len; };   // client_with_order

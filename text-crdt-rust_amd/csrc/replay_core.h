@@ -189,9 +189,9 @@ struct Replayer {
     p(F_FAST, 0);
   }
 
-  CRDT_HD Span* leafp(u32 leaf) const { return lv() + (u64)leaf * L; }
-  CRDT_HD u32* dleaf(u32 blk) const { return dl() + (u64)blk * GROUP; }
-  CRDT_HD u32* dvis(u32 blk) const { return dv() + (u64)blk * GROUP; }
+  CRDT_HD Span* leafp(u32 leaf) const { return w.template at<L>(lv(), leaf); }
+  CRDT_HD u32* dleaf(u32 blk) const { return w.template at<GROUP>(dl(), blk); }
+  CRDT_HD u32* dvis(u32 blk) const { return w.template at<GROUP>(dv(), blk); }
 
   // ------------------------------------------------------------------ init / begin / finish
   // New empty document: ListCRDT::new (doc.rs:51-64): one empty root leaf, frontier [ROOT].
@@ -221,17 +221,17 @@ struct Replayer {
     w.root_load(groups(), g(S_NG));
     u32 n = g(S_N_CWO);
     if (n) {
-      CwoRun r = w.ld_cwo(cwo() + n - 1);
+      CwoRun r = w.ld_cwo(w.at(cwo(), n - 1));
       p(T_CWO_KEY, r.key); p(T_CWO_AGENT, r.agent); p(T_CWO_SEQ, r.seq); p(T_CWO_LEN, r.len);
     }
     n = g(S_N_DEL);
     if (n) {
-      DelRun r = w.ld_del(dels() + n - 1);
+      DelRun r = w.ld_del(w.at(dels(), n - 1));
       p(T_DEL_KEY, r.key); p(T_DEL_ORDER, r.order); p(T_DEL_LEN, r.len);
     }
     n = g(S_N_TXN);
     if (n) {
-      TxnRec t = w.ld_txn(txns() + n - 1);
+      TxnRec t = w.ld_txn(w.at(txns(), n - 1));
       p(T_TX_ORDER, t.order); p(T_TX_LEN, t.len); p(T_TX_SHADOW, t.shadow);
     }
     p(T_FR0, w.ld(fr()));
@@ -239,17 +239,17 @@ struct Replayer {
   // write-back tails -> HBM (the tables' last entries; frontier[0])
   CRDT_HD void flush_tails() {
     u32 n = g(S_N_CWO);
-    if (n) w.st(&cwo()[n - 1].len, g(T_CWO_LEN));
+    if (n) w.st(&w.at(cwo(), n - 1)->len, g(T_CWO_LEN));
     n = g(S_N_DEL);
-    if (n) w.st(&dels()[n - 1].len, g(T_DEL_LEN));
+    if (n) w.st(&w.at(dels(), n - 1)->len, g(T_DEL_LEN));
     n = g(S_N_TXN);
-    if (n) w.st(&txns()[n - 1].len, g(T_TX_LEN));
+    if (n) w.st(&w.at(txns(), n - 1)->len, g(T_TX_LEN));
     flush_agent();
     w.st(fr(), g(T_FR0));
   }
   CRDT_HD void flush_agent() {
     u32 a = g(T_AG_ID), cnt = g(T_AG_CNT);
-    if (a != INVALID && cnt) w.st(&arun()[g(T_AG_BASE) + cnt - 1].len, g(T_AGL_LEN));
+    if (a != INVALID && cnt) w.st(&w.at(arun(), g(T_AG_BASE) + cnt - 1)->len, g(T_AGL_LEN));
   }
   CRDT_HD void finish() {
     commit();
@@ -283,13 +283,13 @@ struct Replayer {
   // The record at pos without moving the window (general path: from HBM when outside it).
   CRDT_HD Rec rec_at(u32 pos) const {
     u32 d = pos - g(T_RB_BASE);
-    return d < 64u ? w.rec_get(d) : w.ld_rec(recs() + pos);
+    return d < 64u ? w.rec_get(d) : w.ld_rec(w.at(recs(), pos));
   }
 
   // ------------------------------------------------------------------ directory
   CRDT_HD void slot_of(u32 leaf, u32& blk, u32& i) const {
     if (leaf == g(C_LEAF)) { blk = g(C_BLK); i = g(C_I); return; }
-    u32 v = w.ld(sol() + leaf);
+    u32 v = w.ld(w.at(sol(), leaf));
     blk = v >> 6;
     i = v & 63u;
   }
@@ -371,7 +371,7 @@ struct Replayer {
   CRDT_HD void ensure(u32 leaf) {
     if (leaf == g(C_LEAF)) return;
     commit();
-    load_cache(leaf, w.ld_raw(sol() + leaf));  // slot and entries: one round trip
+    load_cache(leaf, w.ld_raw(w.at(sol(), leaf)));  // slot and entries: one round trip
   }
   // set entry idx of the cached leaf (tracks the cached visible count exactly)
   CRDT_HD void set(u32 idx, const Span& e) {
@@ -394,7 +394,7 @@ struct Replayer {
   // checks against K_MAP then never trigger for the others).
   CRDT_HD u32 tracked() const { return g(K_MAP) != INVALID; }
   CRDT_HD void map_fill(u32 order, u32 n, u32 v) {
-    if (tracked()) w.fill(lof() + order, n, v);
+    if (tracked()) w.fill(w.at(lof(), order), n, v);
   }
 
   // ------------------------------------------------------------------ cursor ops
@@ -484,7 +484,7 @@ struct Replayer {
       return true;
     }
     if (!tracked()) return false;  // (only remote ops look orders up: the host tracks their documents)
-    u32 lf = w.ld(lof() + order);
+    u32 lf = w.ld(w.at(lof(), order));
     if (lf == INVALID || lf == cl) return false;
     if (load) {
       ensure(lf);
@@ -570,7 +570,7 @@ struct Replayer {
     }
     if (c.off != 0) {
       bool any = false;
-      while (n > 0 && can_append(cur, a0)) {  // append to the entry at the cursor
+      while (n > 0 && can_append_u(cur, a0)) {  // append to the entry at the cursor
         notify(a0, c.leaf, home);
         cur.len += a0.len;
         c.off = slen(cur);
@@ -588,7 +588,7 @@ struct Replayer {
         bool pre = false;
         while (true) {
           Span last = n == 1 ? a0 : (n == 2 ? a1 : a2);
-          if (!can_append(last, nx)) break;
+          if (!can_append_u(last, nx)) break;
           notify(last, c.leaf, home);
           nx.order = last.order;  // YjsSpan::prepend (span.rs:61-64): origin_left is NOT updated
           nx.len += last.len;
@@ -655,13 +655,15 @@ struct Replayer {
     if (a == g(T_AG_ID)) return;
     flush_agent();
     p(T_AG_ID, a);
-    AgentRec r = w.ld_agent(agents() + a);
+    AgentRec r = w.ld_agent(w.at(agents(), a));
     p(T_AG_BASE, r.run_base);
     p(T_AG_CNT, r.run_cnt);
     p(T_AG_CAP, r.run_cap);
     if (r.run_cnt) {
-      ARun x = w.ld_arun(arun() + r.run_base + r.run_cnt - 1);
+      ARun x = w.ld_arun(w.at(arun(), r.run_base + r.run_cnt - 1));
       p(T_AGL_KEY, x.key); p(T_AGL_ORDER, x.order); p(T_AGL_LEN, x.len);
+    } else {
+      p(T_AGL_LEN, 0);  // no runs: the tail test in seq_to_order fails on its own
     }
   }
   CRDT_HD u32 agent_next_seq(u32 agent) {  // doc.rs:20-24
@@ -672,14 +674,14 @@ struct Replayer {
     u32 base, cnt;
     if (agent == g(T_AG_ID)) {
       u32 key = g(T_AGL_KEY);
-      if (g(T_AG_CNT) && seq >= key && seq - key < g(T_AGL_LEN)) {
+      if (seq - key < g(T_AGL_LEN)) {  // (T_AGL_LEN = 0 while the agent has no runs)
         order = g(T_AGL_ORDER) + (seq - key);
         return true;
       }
       base = g(T_AG_BASE);
       cnt = g(T_AG_CNT);
     } else {
-      AgentRec A = w.ld_agent(agents() + agent);
+      AgentRec A = w.ld_agent(w.at(agents(), agent));
       base = A.run_base;
       cnt = A.run_cnt;
     }
@@ -692,24 +694,24 @@ struct Replayer {
   }
   CRDT_HD bool order_to_loc(u32 order, u32& agent, u32& seq) const {  // client_with_order.get() (simple_rle.rs:98-103)
     u32 n = g(S_N_CWO), key = g(T_CWO_KEY);
-    if (n && order >= key && order - key < g(T_CWO_LEN)) {
+    if (order - key < g(T_CWO_LEN)) {  // (T_CWO_LEN = 0 while the table is empty)
       agent = g(T_CWO_AGENT);
       seq = g(T_CWO_SEQ) + (order - key);
       return true;
     }
     i32 k = w.search_cwo(cwo(), n, order);
     if (k < 0) return false;
-    CwoRun r = w.ld_cwo(cwo() + k);
+    CwoRun r = w.ld_cwo(w.at(cwo(), (u32)k));
     agent = r.agent;
     seq = r.seq + (order - r.key);
     return true;
   }
   CRDT_HD bool order_to_agent(u32 order, u32& agent) const {  // client_with_order.get()
     u32 n = g(S_N_CWO), key = g(T_CWO_KEY);
-    if (n && order >= key && order - key < g(T_CWO_LEN)) { agent = g(T_CWO_AGENT); return true; }
+    if (order - key < g(T_CWO_LEN)) { agent = g(T_CWO_AGENT); return true; }
     i32 k = w.search_cwo(cwo(), n, order);
     if (k < 0) return false;
-    agent = w.ld_cwo(cwo() + k).agent;
+    agent = w.ld_cwo(w.at(cwo(), (u32)k)).agent;
     return true;
   }
   // doc.rs:155-165 assign_order_to_client
@@ -719,9 +721,9 @@ struct Replayer {
     if (n > 0 && order == ck + cl && agent == g(T_CWO_AGENT) && seq == g(T_CWO_SEQ) + cl) {
       p(T_CWO_LEN, cl + len);
     } else {
-      if (n) w.st(&cwo()[n - 1].len, cl);  // retire the old tail
+      if (n) w.st(&w.at(cwo(), n - 1)->len, cl);  // retire the old tail
       p(T_CWO_KEY, order); p(T_CWO_AGENT, agent); p(T_CWO_SEQ, seq); p(T_CWO_LEN, len);
-      w.st_cwo(cwo() + n, CwoRun{order, agent, seq, len});
+      w.st_cwo(w.at(cwo(), n), CwoRun{order, agent, seq, len});
       p(S_N_CWO, n + 1);
     }
     use_agent(agent);
@@ -730,23 +732,27 @@ struct Replayer {
     if (an > 0 && seq == lk + ll && order == g(T_AGL_ORDER) + ll) {
       p(T_AGL_LEN, ll + len);
     } else {
-      if (an) w.st(&arun()[base + an - 1].len, ll);
+      if (an) w.st(&w.at(arun(), base + an - 1)->len, ll);
       p(T_AGL_KEY, seq); p(T_AGL_ORDER, order); p(T_AGL_LEN, len);
-      w.st_arun(arun() + base + an, ARun{seq, order, len, 0});
+      w.st_arun(w.at(arun(), base + an), ARun{seq, order, len, 0});
       p(T_AG_CNT, an + 1);
-      w.st(&agents()[agent].run_cnt, an + 1);
+      w.st(&w.at(agents(), agent)->run_cnt, an + 1);
     }
   }
   CRDT_HD void append_delete(u32 key, u32 target, u32 len) {  // Rle<KVPair<DeleteEntry>>::append
     u32 n = g(S_N_DEL);
     u32 dk = g(T_DEL_KEY), dlen = g(T_DEL_LEN);
-    if (n > 0 && key == dk + dlen && g(T_DEL_ORDER) + dlen == target) {
-      p(T_DEL_LEN, dlen + len);
-      return;
+    if (n != 0u) {
+      if (key == dk + dlen) {
+        if (g(T_DEL_ORDER) + dlen == target) {
+          p(T_DEL_LEN, dlen + len);
+          return;
+        }
+      }
     }
-    if (n) w.st(&dels()[n - 1].len, dlen);
+    if (n) w.st(&w.at(dels(), n - 1)->len, dlen);
     p(T_DEL_KEY, key); p(T_DEL_ORDER, target); p(T_DEL_LEN, len);
-    w.st_del(dels() + n, DelRun{key, target, len});
+    w.st_del(w.at(dels(), n), DelRun{key, target, len});
     p(S_N_DEL, n + 1);
   }
   // ---- double_deletes: an RLE of DDRun in 64-entry blocks (crdt_types.h DDBlk).  A position is
@@ -915,18 +921,18 @@ struct Replayer {
       if (ntx && x >= txo && x - txo < txl) { shadow = txs; continue; }
       i32 k = w.search_txn(txns(), ntx, x);
       if (k < 0) return ST_UNKNOWN_ID;
-      shadow = w.ld(&txns()[k].shadow);
+      shadow = w.ld(&w.at(txns(), (u32)k)->shadow);
     }
     if (ntx > 0 && np == 1 && p0 == txo + txl - 1 && shadow == txs) {
       p(T_TX_LEN, txl + len);  // write-back: the merged length reaches HBM with the tail
       return ST_OK;            // parents of a merged txn are not kept
     }
     if (np) w.st(pp, p0);
-    if (ntx) w.st(&txns()[ntx - 1].len, txl);  // retire the old tail
+    if (ntx) w.st(&w.at(txns(), ntx - 1)->len, txl);  // retire the old tail
     p(T_TX_ORDER, first);
     p(T_TX_LEN, len);
     p(T_TX_SHADOW, shadow);
-    w.st_txn(txns() + ntx, TxnRec{first, len, shadow, npar, np, {0, 0, 0}});
+    w.st_txn(w.at(txns(), ntx), TxnRec{first, len, shadow, npar, np, {0, 0, 0}});
     p(S_N_TXN, ntx + 1);
     p(S_N_PAR, npar + np);
     return ST_OK;
@@ -1102,8 +1108,8 @@ struct Replayer {
           if (r == 0) {
             u32 oa;
             if (!order_to_agent(oe.order, oa)) return ST_UNKNOWN_ID;
-            u32 my_rank = w.ld(&agents()[agent].rank);
-            u32 other_rank = w.ld(&agents()[oa].rank);
+            u32 my_rank = w.ld(&w.at(agents(), agent)->rank);
+            u32 other_rank = w.ld(&w.at(agents(), oa)->rank);
             if (my_rank > other_rank) scanning = false;
             else if (item.orr == oe.orr) break;
             else { scanning = true; scan_start = c; }
@@ -1205,14 +1211,26 @@ struct Replayer {
   // A fast commit (fast_txn_commit) extends every one of these tails by the txn, so after it all
   // conditions that do not name the next txn's author and seq still hold (F_FAST); only
   // apply_txn changes them otherwise.  Then the check is: same author, next seq.
+  //
+  // Conditions are written as early exits throughout the fast paths: each is one s_cmp and one
+  // branch, where an `a & b & ...` chain of uniform compares becomes 64-bit lane masks (s_cmp,
+  // s_cselect_b64, s_and_b64 per term) on the scalar unit this kernel is bound by.
   CRDT_HD u32 fast_txn_ok(u32 agent, u32 seq, u32 first) const {
+    if (agent != g(T_AG_ID)) return 0;
     u32 ll = g(T_AGL_LEN);
-    if (g(F_FAST)) return (agent == g(T_AG_ID)) & (seq == g(T_AGL_KEY) + ll);
+    if (seq != g(T_AGL_KEY) + ll) return 0;
+    if (g(F_FAST)) return 1;
+    if (g(T_AG_CNT) == 0u) return 0;
+    if (g(T_AGL_ORDER) + ll != first) return 0;
+    if (g(S_N_CWO) == 0u) return 0;
+    if (g(T_CWO_AGENT) != agent) return 0;
     u32 cl = g(T_CWO_LEN);
-    return (agent == g(T_AG_ID)) & (g(T_AG_CNT) != 0u) & (seq == g(T_AGL_KEY) + ll) &
-           (g(T_AGL_ORDER) + ll == first) & (g(S_N_CWO) != 0u) & (g(T_CWO_AGENT) == agent) &
-           (g(T_CWO_SEQ) + cl == seq) & (g(T_CWO_KEY) + cl == first) & (g(S_N_FR) == 1u) &
-           (g(T_FR0) == first - 1u) & (g(S_N_TXN) != 0u) & (g(T_TX_ORDER) + g(T_TX_LEN) == first);
+    if (g(T_CWO_SEQ) + cl != seq) return 0;
+    if (g(T_CWO_KEY) + cl != first) return 0;
+    if (g(S_N_FR) != 1u) return 0;
+    if (g(T_FR0) != first - 1u) return 0;
+    if (g(S_N_TXN) == 0u) return 0;
+    return g(T_TX_ORDER) + g(T_TX_LEN) == first;
   }
   CRDT_HD void fast_txn_commit(u32 first, u32 len) {
     p(S_NEXT_ORDER, first + len);
@@ -1251,7 +1269,7 @@ struct Replayer {
       u32 last = pos0 + (nt - 1u) * per;
       u32 n = rn - last < 64u ? rn - last : 64u;
       u32 t2, l0;
-      u32 n2 = w.typing_scan_at(recs() + last, n, remote, cpt, agent, ow1, o.w3, t2, l0);
+      u32 n2 = w.typing_scan_at(w.at(recs(), last), n, remote, cpt, agent, ow1, o.w3, t2, l0);
       end = last + n;
       if (n2 <= 1u) break;
       total += t2 - l0;
@@ -1290,7 +1308,7 @@ struct Replayer {
     if (m != 0u && idx + 1u < n) {
       nx = w.cget(idx + 1u);
       Span last = m == 2u ? pc : x0;
-      if (can_append(last, nx)) {
+      if (can_append_u(last, nx)) {
         nx.order = last.order;  // YjsSpan::prepend keeps origin_left (span.rs:61-64)
         nx.len += last.len;
         pre = 1;
@@ -1314,7 +1332,7 @@ struct Replayer {
   //    either prepends it onto the entry after E or inserts it there.  A fresh single deleted item
   //    {t, t-1} accepts the next one (YjsSpan::can_append), after which its origin_left equals
   //    its order (span.rs:61-64) and it accepts no more: new entries alternate insert / prepend,
-  //    starting with a prepend onto the next entry N0 iff can_append(first deleted item, N0);
+  //    starting with a prepend onto the next entry N0 iff can_append_u(first deleted item, N0);
   //  * forward deleting from item `off` of E (the remainder never prepends onto the next
   //    entry): E becomes [E[..off]] [k single deleted items] [the rest of E].
   // Returns k' <= k deletes applied (0: not this shape / no room; nothing changed).
@@ -1328,7 +1346,7 @@ struct Replayer {
     u32 delta;
     if (back) {
       if (off + 1u != (u32)E.len) return 0;  // not from the entry's last item
-      u32 p0 = has_nx && can_append(Span{t1, t1 - 1u, orr, -1}, N0);
+      u32 p0 = has_nx && can_append_u(Span{t1, t1 - 1u, orr, -1}, N0);
       u32 kmax = 2u * room + p0;
       k = k < off ? k : off;  // E keeps its first item (deleting it is a different shape)
       k = k < kmax ? k : kmax;
@@ -1346,7 +1364,7 @@ struct Replayer {
       w.cset(idx, E);
     } else {
       u32 ha = off > 0u;
-      if (has_nx && can_append(Span{t1 + 1u, t1, orr, E.len - (i32)off - 1}, N0)) return 0;
+      if (has_nx && can_append_u(Span{t1 + 1u, t1, orr, E.len - (i32)off - 1}, N0)) return 0;
       u32 kmax = room > ha ? room - ha : 0u;  // adds ha + k entries with a remainder (one fewer without)
       k = k < kmax ? k : kmax;
       if (k < 2u) return 0;
@@ -1383,19 +1401,26 @@ struct Replayer {
       if (m && idx + 1u < n) {
         Span last = hc ? Span{t1 + l, t1 + l - 1u, e.orr, e.len - (i32)(off + l)}
                        : Span{t1, ha ? t1 - 1u : e.ol, e.orr, -(i32)l};
-        m -= can_append(last, w.cget(idx + 1u));
+        m -= can_append_u(last, w.cget(idx + 1u));
       }
       if (n + m > (u32)L) return 0;  // a leaf split: the general path's job
     }
     u32 k = 1, back = 0;
     u32 key = g(T_AGL_KEY);
-    u32 in_run = !remote || (((o.w1 & 0xFFFFu) == agent) & (o.w2 - key < g(T_AGL_LEN)));
-    if ((l == 1u) & (b0 + 2u * per <= nv) & in_run) {
+    do {  // a run of one-item deletes follows?  (early exits: see fast_txn_ok)
+      if (l != 1u) break;
+      if (b0 + 2u * per > nv) break;
+      if (remote) {
+        if ((o.w1 & 0xFFFFu) != agent) break;
+        if (o.w2 - key >= g(T_AGL_LEN)) break;
+      }
       Rec o2 = op_at(b0 + per, remote);
       u32 delta = remote ? o2.w2 - o.w2 : o2.w1 - o.w1;
-      back = delta == 0xFFFFFFFFu;
-      u32 fwd = delta == (remote ? 1u : 0u);
-      if (back | fwd) {
+      back = opq(delta == 0xFFFFFFFFu ? 1u : 0u);
+      if (!back) {
+        if (delta != (remote ? 1u : 0u)) break;
+      }
+      {
         u32 room = back ? off + 1u : (u32)w.cget_len(idx) - off;  // targets stay in this entry
         if (remote) {  // ... and in the author's last item_orders run (contiguous orders)
           u32 r2 = back ? o.w2 - key + 1u : key + g(T_AGL_LEN) - o.w2;
@@ -1409,7 +1434,7 @@ struct Replayer {
         while ((k < room) & (pos0 + (k + 1u) * per > end) & (end < rn)) {
           u32 last = pos0 + (k - 1u) * per;
           u32 n = rn - last < 64u ? rn - last : 64u;
-          u32 n2 = w.delete_scan_at(recs() + last, n, remote, cpt, agent, delta);
+          u32 n2 = w.delete_scan_at(w.at(recs(), last), n, remote, cpt, agent, delta);
           end = last + n;
           if (n2 <= 1u) break;
           k += n2 - 1u;
@@ -1419,18 +1444,20 @@ struct Replayer {
 #endif
         k = k < room ? k : room;
       }
-    }
+    } while (0);
 #ifdef CRDT_PROF
     if (prof_mode == 3u) { inc(S_PROF3); if (k == 1u) inc(S_PROF2); }  // detail: delete calls, single deletes
 #endif
-    if ((g(K_MAP) - first < k * l) | (g(K_DEL) - g(S_N_DEL) < k)) return 0;
+    if (g(K_MAP) - first < k * l) return 0;
+    if (g(K_DEL) - g(S_N_DEL) < k) return 0;
     u32 done = k >= 2u ? delete_run_closed(idx, off, t1, k, back) : 0u;
     if (done == 0u) {  // op by op
       for (u32 j = 0; j < k; j++) {
         u32 ij = back ? idx : (j == 0u ? idx : idx + (off > 0u) + j);  // forward: the remainder moves right
         u32 oj = back ? off - j : (j == 0u ? off : 0u);
         u32 tj = back ? t1 - j : t1 + j;
-        if ((w.cget_order(ij) + oj != tj) | (w.cget_len(ij) <= (i32)oj)) break;
+        if (w.cget_order(ij) + oj != tj) break;
+        if (w.cget_len(ij) <= (i32)oj) break;
         if (!leaf_delete(ij, oj, l)) break;
         done++;
       }
@@ -1443,8 +1470,8 @@ struct Replayer {
       append_delete(first, t1, 1u);
       if (done > 1u) {
         u32 n = g(S_N_DEL);
-        w.st(&dels()[n - 1u].len, g(T_DEL_LEN));  // retire the tail
-        w.st_del_run(dels() + n, done - 1u, first + 1u, t1 - 1u);
+        w.st(&w.at(dels(), n - 1u)->len, g(T_DEL_LEN));  // retire the tail
+        w.st_del_run(w.at(dels(), n), done - 1u, first + 1u, t1 - 1u);
         p(S_N_DEL, n + done - 1u);
         p(T_DEL_KEY, first + done - 1u);
         p(T_DEL_ORDER, t1 - (done - 1u));
@@ -1487,8 +1514,9 @@ struct Replayer {
   // gen: a txn expanded from a GEN record (header gh, op go; no record window, no runs).
   // kind: the record kind at `pos` (RTXN / LTXN / RC / LC; LTXN for a generated op).
   CRDT_HD u32 fast_txn(u32 pos, u32 kind, u32 gen, const Rec& gh, const Rec& go) {
-    cpt = (kind == REC_RC) | (kind == REC_LC);
-    u32 remote = (kind == REC_RTXN) | (kind == REC_RC);
+    // set membership by bitmask: no lane-mask booleans
+    cpt = ((1u << REC_RC | 1u << REC_LC) >> kind) & 1u;
+    u32 remote = ((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u;
     u32 per = per_txn(remote);
     u32 rn = rec_n();
     if (g(C_LEAF) == INVALID) return 0;
@@ -1529,8 +1557,11 @@ struct Replayer {
         return 0;
       }
       if (!fast_txn_ok(agent, seq, first)) return 0;
-      if (id_to_order(o.w1 & 0xFFFFu, o.w2, ol) != ST_OK || ol == ROOT_ORDER) return 0;  // origin_left / target
-      if (ins && id_to_order(o.w1 >> 16, o.w3, orr) != ST_OK) return 0;
+      if (id_to_order(o.w1 & 0xFFFFu, o.w2, ol) != ST_OK) return 0;  // origin_left / target
+      if (ol == ROOT_ORDER) return 0;
+      if (ins) {
+        if (id_to_order(o.w1 >> 16, o.w3, orr) != ST_OK) return 0;
+      }
       if (!find_order(ol, true, c)) return 0;  // doc.rs:101-136 (loads the item's leaf)
       c.off += ins;                             // get_cursor_after
     } else {
@@ -1538,9 +1569,16 @@ struct Replayer {
       u32 lp = o.w1, del = o.w2;
       ins = o.w3 != 0u;
       l = del + o.w3;
-      u32 ok = ((del != 0u) != ins) & (l - 1u < 0xFFFFu) & ((lp != 0u) | !ins);
-      if (gen_form) ok &= (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l);
-      if (!ok || !fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first)) return 0;
+      if ((del != 0u) == ins) return 0;
+      if (l - 1u >= 0xFFFFu) return 0;
+      if (ins) {
+        if (lp == 0u) return 0;
+      }
+      if (gen_form) {
+        u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l);
+        if (!ok) return 0;
+      }
+      if (!fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first)) return 0;
       if (!cursor_at_content_pos(ins ? lp - 1u : lp, c)) return 0;  // root.rs:54-88 (loads the leaf)
       ol = w.cget_order(c.idx) + c.off;  // doc.rs:446-449: the item at pos - 1, then Cursor::next
       c.off += ins;
@@ -1551,16 +1589,20 @@ struct Replayer {
       if (c.off < el) { nxo = w.cget_order(idx) + c.off; has = 1; }
       else has = next_item_after(idx, nxo);
       if (remote) {
-        if (has && nxo != orr) return 0;  // integrate would scan (doc.rs:183-221)
+        if (has) {
+          if (nxo != orr) return 0;  // integrate would scan (doc.rs:183-221)
+        }
       } else {
         orr = has ? nxo : ROOT_ORDER;  // doc.rs:453; integrate then stops at once
       }
       Span item{first, ol, orr, (i32)l};
       Span e = w.cget(idx);
 #ifdef CRDT_PROF
-      prof_cat = ((c.off == el) & can_append(e, item)) ? 0u : 3u;
+      prof_cat = ((c.off == el) & can_append_u(e, item)) ? 0u : 3u;
 #endif
-      if ((c.off == el) & can_append(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
+      if (c.off == el) {
+        if (can_append_u(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
+      }
       // no room for the item (+ the entry's remainder): a leaf split, the general path's job
       if (g(C_N) + 1u + (c.off < el) > (u32)L) {
         pre = 1;
@@ -1577,7 +1619,8 @@ struct Replayer {
       return nt * per;
     }
     i32 el = w.cget_len(idx);
-    if ((el <= 0) | (c.off + l > (u32)el)) return 0;  // already deleted / spans entries
+    if (el <= 0) return 0;                // already deleted
+    if (c.off + l > (u32)el) return 0;    // spans entries
 #ifdef CRDT_PROF
     prof_cat = 2u;
 #endif
@@ -1626,7 +1669,7 @@ struct Replayer {
     while (pos < rn) {
       Rec h = rec(pos);
       u32 kind = rec_kind(h);
-      u32 gen = kind == REC_GEN;
+      u32 gen = opq(kind == REC_GEN ? 1u : 0u);
       Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
       u32 inl = 0;
       if (gen) {
@@ -1639,7 +1682,7 @@ struct Replayer {
       }
       i32 st;
       u32 consumed;
-      if (kind == REC_LTXN || kind == REC_RTXN || kind == REC_RC || kind == REC_LC) {
+      if (((1u << REC_LTXN | 1u << REC_RTXN | 1u << REC_RC | 1u << REC_LC) >> kind) & 1u) {
 #ifdef CRDT_PROF
         u64 t0 = w.clock();
 #endif
@@ -1658,7 +1701,7 @@ struct Replayer {
           else pos += fast;
           continue;
         }
-        bool remote = kind == REC_RTXN || kind == REC_RC;
+        bool remote = ((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u;
         if (kind == REC_RC) { expand_rc(h, h, gop, gpar); inl = 1; }
         if (kind == REC_LC) { expand_lc(h, h, gop); inl = 1; }
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
