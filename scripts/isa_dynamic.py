@@ -255,7 +255,8 @@ def main():
         for (a, mn, _), (fl, ln, ch) in zip(blk, info):
             if mn.startswith(("s_nop", "s_waitcnt")):
                 continue
-            kind = ("branch" if mn.startswith(("s_cbranch", "s_branch")) else "salu" if mn.startswith("s_")
+            kind = ("branch" if mn.startswith(("s_cbranch", "s_branch")) else "scratch" if mn.startswith("scratch_")
+                    else "salu" if mn.startswith("s_")
                     else "lane" if mn.startswith(("v_readlane", "v_writelane", "v_readfirstlane"))
                     else "valu" if mn.startswith("v_") else "mem")
             fn = ch[-1].name if ch else SYM

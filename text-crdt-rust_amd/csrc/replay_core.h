@@ -1686,7 +1686,12 @@ struct Replayer {
 #ifdef CRDT_PROF
         u64 t0 = w.clock();
 #endif
-        u32 fast = fast_txn(pos, kind, gen, h, gop);
+        // compact remote txns (the remote-batch hot path) get their own instance of the fast paths,
+        // with record kind, format and stride known at compile time
+        // (also the compact local form and generated ops: the other batch shapes)
+        u32 fast = kind == REC_RC ? fast_txn(pos, REC_RC, 0u, h, gop)
+                 : kind == REC_LC ? fast_txn(pos, REC_LC, 0u, h, gop)
+                 : gen ? fast_txn(pos, REC_LTXN, 1u, h, gop) : fast_txn(pos, kind, 0u, h, gop);
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
         u32 dt = prof_mode == 0u ? (u32)(t1 - t0) : prof_mode == 1u ? 1u : (fast ? fast / per_txn(kind == REC_RTXN || kind == REC_RC) : 0u);
