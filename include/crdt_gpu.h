@@ -74,6 +74,14 @@ uint64_t crdt_num_docs(const crdt_engine* e);
 /* ListCRDT::get_or_create_agent_id (doc.rs:66-80), n independent (doc, name) requests. */
 int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const char* const* names,
                       uint16_t* agent_out);
+/* The same interning done by a device kernel (one wave per document): name i is
+ * the bytes [name_off[i], name_off[i+1]) of `bytes` (any bytes, not NUL-terminated).  Ids are
+ * identical to crdt_agent_intern on the same call.  rank_out (optional): each name's rank among
+ * the document's names in byte-lexicographic order (Rust str Ord; the order the integrate
+ * tie-break compares, doc.rs:207), INVALID for "ROOT".  At most 1024 names per document
+ * (CRDT_E_ARG beyond). */
+int crdt_agent_intern_dev(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint64_t* name_off,
+                          const char* bytes, uint16_t* agent_out, uint32_t* rank_out);
 
 /* ListCRDT::apply_local_txn (doc.rs:376-469) for many documents.  Document docs[i] applies txns
  * txns[txn_off[i] .. txn_off[i+1]) in order; ops are concatenated in txn order. */

@@ -76,6 +76,7 @@ def lib():
     L.crdt_num_docs.argtypes = [vp]
     L.crdt_num_docs.restype = u64
     L.crdt_agent_intern.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(C.c_uint16)]
+    L.crdt_agent_intern_dev.argtypes = [vp, u64, P(u32), P(u64), C.c_char_p, P(C.c_uint16), P(u32)]
     L.crdt_apply_local.argtypes = [vp, u64, P(u32), P(u64), vp, vp, P(i32)]
     L.crdt_stage_local.argtypes = [vp, u64, P(u32), P(u64), vp, vp]
     L.crdt_apply_remote_wire.argtypes = [vp, u64, P(u32), P(C.c_char_p), P(u64), P(i32)]
@@ -124,7 +125,7 @@ def lib():
 
 
 EXPORTED_SYMBOLS = [
-    "crdt_engine_create", "crdt_engine_destroy", "crdt_docs_alloc", "crdt_num_docs", "crdt_agent_intern",
+    "crdt_engine_create", "crdt_engine_destroy", "crdt_docs_alloc", "crdt_num_docs", "crdt_agent_intern", "crdt_agent_intern_dev",
     "crdt_apply_local", "crdt_apply_remote_wire", "crdt_stage_local", "crdt_stage_remote_wire",
     "crdt_stage_remote_replicated", "crdt_reset_async", "crdt_run", "crdt_run_async", "crdt_publish_async",
     "crdt_sync", "crdt_pos_to_loc", "crdt_loc_to_pos", "crdt_pos_to_loc_dev_async", "crdt_loc_to_pos_dev_async",
@@ -178,6 +179,20 @@ class Engine:
         out = np.zeros(len(names), np.uint16)
         _check(self.L.crdt_agent_intern(self.h, len(names), _p(d), arr, _p(out, C.c_uint16)), "agent_intern")
         return out
+
+    def agent_intern_dev(self, docs: Sequence[int], names: Sequence) -> tuple:
+        """get_or_create_agent_id on the device (k_intern): (ids u16, ranks u32) per name; names
+        are str or bytes (any bytes).  Same ids as agent_intern on the same call."""
+        d = np.ascontiguousarray(docs, dtype=np.uint32)
+        bs = [n.encode() if isinstance(n, str) else bytes(n) for n in names]
+        off = np.zeros(len(bs) + 1, np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs]) if bs else []
+        blob = b"".join(bs)
+        out = np.zeros(len(bs), np.uint16)
+        rank = np.zeros(len(bs), np.uint32)
+        _check(self.L.crdt_agent_intern_dev(self.h, len(bs), _p(d), _p(off, C.c_uint64), blob, _p(out, C.c_uint16),
+                                            _p(rank)), "agent_intern_dev")
+        return out, rank
 
     @staticmethod
     def _local_arrays(per_doc):

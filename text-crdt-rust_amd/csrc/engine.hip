@@ -953,6 +953,99 @@ int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const cha
   return 0;
 }
 
+// Device interning (kernels.h k_intern): the same results as crdt_agent_intern on the same call.
+// Each document named in the call forms one group: its existing names (in id order, so the
+// first-appearance numbering reproduces their ids) followed by this call's names for it.
+int crdt_agent_intern_dev(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint64_t* name_off,
+                          const char* bytes, uint16_t* out, uint32_t* rank_out) {
+  if (!valid(e) || (n && (!doc || !name_off || !bytes || !out))) return CRDT_E_ARG;
+  if (!n) return 0;
+  std::vector<u32> group_of_doc;  // doc -> group + 1 (sparse via map for large engines)
+  std::unordered_map<u32, u32> gmap;
+  std::vector<u32> gdoc;
+  std::vector<std::vector<u64>> grefs;  // per group: call refs (indices into the call)
+  for (u64 i = 0; i < n; i++) {
+    if (doc[i] >= e->n_docs || name_off[i + 1] < name_off[i]) return CRDT_E_ARG;
+    auto it = gmap.find(doc[i]);
+    u32 g;
+    if (it == gmap.end()) { g = (u32)gdoc.size(); gmap[doc[i]] = g; gdoc.push_back(doc[i]); grefs.emplace_back(); }
+    else g = it->second;
+    grefs[g].push_back(i);
+  }
+  // blob: per group the existing names, then the call's names
+  std::vector<unsigned char> blob;
+  std::vector<u32> noff{0};
+  std::vector<u64> roff{0};
+  std::vector<u64> call_ref(n);  // call index -> ref index
+  for (u32 g = 0; g < gdoc.size(); g++) {
+    const AgentTable& t = e->docs[gdoc[g]].agents;
+    for (const std::string& nm : t.names) {
+      blob.insert(blob.end(), nm.begin(), nm.end());
+      noff.push_back((u32)blob.size());
+    }
+    for (u64 i : grefs[g]) {
+      call_ref[i] = noff.size() - 1;
+      blob.insert(blob.end(), bytes + name_off[i], bytes + name_off[i + 1]);
+      if (blob.size() >= 0xFFFFFFFFull) return CRDT_E_ARG;
+      noff.push_back((u32)blob.size());
+    }
+    roff.push_back(noff.size() - 1);
+  }
+  u64 nr = noff.size() - 1, ng = gdoc.size();
+  u64 sz = blob.size() + 16 + noff.size() * 4 + roff.size() * 8 + nr * (2 + 4) + ng * 8 + 256;
+  int r = e->scratch(sz);
+  if (r) return r;
+  char* q = (char*)e->qbuf;
+  auto carve = [&](u64 bytes_) { char* p = q; q += (bytes_ + 15) & ~15ull; return p; };
+  u64* d_roff = (u64*)carve(roff.size() * 8);
+  u32* d_noff = (u32*)carve(noff.size() * 4);
+  u32* d_rank = (u32*)carve(nr * 4);
+  u32* d_n = (u32*)carve(ng * 4);
+  i32* d_st = (i32*)carve(ng * 4);
+  u16* d_id = (u16*)carve(nr * 2);
+  unsigned char* d_b = (unsigned char*)carve(blob.size() + 1);
+  HIPCHK(hipMemcpyAsync(d_roff, roff.data(), roff.size() * 8, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipMemcpyAsync(d_noff, noff.data(), noff.size() * 4, hipMemcpyHostToDevice, e->stream));
+  if (!blob.empty()) HIPCHK(hipMemcpyAsync(d_b, blob.data(), blob.size(), hipMemcpyHostToDevice, e->stream));
+  InternIO io{d_roff, d_noff, d_b, d_id, d_rank, d_n, d_st};
+  hipLaunchKernelGGL(k_intern, dim3((u32)ng), dim3(64), 0, e->stream, io, (u32)ng);
+  HIPCHK(hipGetLastError());
+  std::vector<u16> id(nr);
+  std::vector<u32> rank(nr), gn(ng);
+  std::vector<i32> gst(ng);
+  HIPCHK(hipMemcpyAsync(id.data(), d_id, nr * 2, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(rank.data(), d_rank, nr * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(gn.data(), d_n, ng * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipMemcpyAsync(gst.data(), d_st, ng * 4, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (u32 g = 0; g < ng; g++) {
+    if (gst[g] != 0) {
+      g_last_error = "crdt_agent_intern_dev: more than 1024 distinct names in one document";
+      return CRDT_E_ARG;
+    }
+  }
+  // mirror the new names into the host tables (capacity planning, host lookups), in id order
+  for (u32 g = 0; g < ng; g++) {
+    AgentTable& t = e->docs[gdoc[g]].agents;
+    u32 old = (u32)t.names.size();
+    for (u64 ref = roff[g]; ref < roff[g] + old; ref++)
+      if (id[ref] != ref - roff[g]) { g_last_error = "crdt_agent_intern_dev: existing id mismatch"; return CRDT_E_DEVICE; }
+    for (u64 ref = roff[g] + old; ref < roff[g + 1]; ref++) {
+      if (id[ref] == (u16)t.names.size()) {
+        std::string nm((const char*)blob.data() + noff[ref], noff[ref + 1] - noff[ref]);
+        t.ids[nm] = id[ref];
+        t.names.push_back(nm);
+      }
+    }
+    if (t.names.size() != gn[g]) { g_last_error = "crdt_agent_intern_dev: name count mismatch"; return CRDT_E_DEVICE; }
+  }
+  for (u64 i = 0; i < n; i++) {
+    out[i] = id[call_ref[i]];
+    if (rank_out) rank_out[i] = rank[call_ref[i]];
+  }
+  return 0;
+}
+
 // probes (optional): one per txn, encoded after it; probe_rec gets each probe's record index
 static int stage_local_impl(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
                             const crdt_local_txn* txns, const crdt_local_op* ops,

@@ -779,4 +779,107 @@ __global__ void k_loc_to_pos(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* d
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Agent-name interning on the device (ListCRDT::get_or_create_agent_id, doc.rs:66-89; SURVEY
+// §8f row 3).  One wave per group (a document's name references in call order): ids in order of
+// first appearance ("ROOT" -> ROOT_AGENT, never stored), and every distinct name's rank in
+// byte-lexicographic order (Rust `str` Ord, the integrate tie-break's order, doc.rs:207).
+// Group g owns refs [roff[g], roff[g+1]); ref r names bytes [noff[r], noff[r+1]).  A wave hashes
+// 64 refs at once (FNV-1a), looks them up in an LDS open-addressing table, and admits the new
+// names of the chunk one distinct name per step in lane order (the first appearance leads).
+// ---------------------------------------------------------------------------------------------
+constexpr u32 INTERN_MAX = 1024, INTERN_HT = 2 * INTERN_MAX;
+struct InternIO {
+  const u64* roff;
+  const u32* noff;
+  const unsigned char* bytes;
+  u16* id;      // per ref
+  u32* rank;    // per ref (INVALID for ROOT)
+  u32* n_out;   // per group: distinct names
+  i32* status;  // per group: 0, or -1 when a group has more than INTERN_MAX distinct names
+};
+__device__ __forceinline__ bool intern_eq(const unsigned char* b, u32 a0, u32 a1, u32 c0, u32 c1) {
+  if (a1 - a0 != c1 - c0) return false;
+  for (u32 i = 0; i < a1 - a0; i++)
+    if (b[a0 + i] != b[c0 + i]) return false;
+  return true;
+}
+__device__ __forceinline__ bool intern_less(const unsigned char* b, u32 a0, u32 a1, u32 c0, u32 c1) {
+  u32 la = a1 - a0, lc = c1 - c0, m = la < lc ? la : lc;
+  for (u32 i = 0; i < m; i++) {
+    unsigned char x = b[a0 + i], y = b[c0 + i];
+    if (x != y) return x < y;
+  }
+  return la < lc;
+}
+__global__ __launch_bounds__(64) void k_intern(InternIO io, u32 n_groups) {
+  __shared__ u32 ht[INTERN_HT];      // 0 = empty, else id + 1
+  __shared__ u32 hh[INTERN_HT];      // hash of the slot's name
+  __shared__ u32 rep[INTERN_MAX];    // a ref naming each id (its first appearance)
+  __shared__ u32 rk[INTERN_MAX];     // rank of each id
+  u32 g = blockIdx.x, l = threadIdx.x;
+  if (g >= n_groups) return;
+  for (u32 i = l; i < INTERN_HT; i += 64) ht[i] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  const unsigned char* B = io.bytes;
+  u64 r0 = io.roff[g], r1 = io.roff[g + 1];
+  u32 k = 0;
+  i32 st = 0;
+  for (u64 c = r0; c < r1 && st == 0; c += 64) {
+    u64 r = c + l;
+    bool v = r < r1;
+    u32 a = v ? io.noff[r] : 0u, b = v ? io.noff[r + 1] : 0u;
+    u32 h = 2166136261u;
+    for (u32 i = a; i < b; i++) h = (h ^ B[i]) * 16777619u;
+    bool root = v && b - a == 4u && B[a] == 'R' && B[a + 1] == 'O' && B[a + 2] == 'O' && B[a + 3] == 'T';
+    u32 id = INVALID;
+    if (v && !root) {  // lookup
+      for (u32 s = h & (INTERN_HT - 1u);; s = (s + 1u) & (INTERN_HT - 1u)) {
+        u32 e = ht[s];
+        if (e == 0u) break;
+        if (hh[s] == h && intern_eq(B, a, b, io.noff[rep[e - 1u]], io.noff[rep[e - 1u] + 1u])) { id = e - 1u; break; }
+      }
+    }
+    u64 need = __builtin_amdgcn_ballot_w64(v && !root && id == INVALID);
+    while (need) {  // admit the chunk's new names, first appearance first
+      u32 ld = (u32)__builtin_ctzll(need);
+      u32 lh = __builtin_amdgcn_readlane(h, ld), la = __builtin_amdgcn_readlane(a, ld), lb = __builtin_amdgcn_readlane(b, ld);
+      if (k >= INTERN_MAX) { st = -1; break; }
+      bool mine = (need >> l) & 1ull;
+      bool same = mine && h == lh && intern_eq(B, a, b, la, lb);
+      if (same) id = k;
+      if (l == ld) {
+        u32 s = h & (INTERN_HT - 1u);
+        while (ht[s] != 0u) s = (s + 1u) & (INTERN_HT - 1u);
+        ht[s] = k + 1u;
+        hh[s] = h;
+        rep[k] = (u32)r;
+      }
+      __builtin_amdgcn_wave_barrier();
+      k++;
+      need &= ~__builtin_amdgcn_ballot_w64(same);
+    }
+    if (v) io.id[r] = (u16)(root ? ROOT_AGENT : id);
+  }
+  __builtin_amdgcn_wave_barrier();
+  // ranks: names smaller than each distinct name (lane per name)
+  for (u32 i = l; i < k; i += 64) {
+    u32 ra = rep[i], a = io.noff[ra], b = io.noff[ra + 1], cnt = 0;
+    for (u32 j = 0; j < k; j++) {
+      u32 rj = rep[j];
+      cnt += intern_less(B, io.noff[rj], io.noff[rj + 1], a, b) ? 1u : 0u;
+    }
+    rk[i] = cnt;
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (u64 r = r0 + l; r < r1; r += 64) {
+    u32 id = io.id[r];
+    io.rank[r] = (id == ROOT_AGENT || id >= k) ? INVALID : rk[id];
+  }
+  if (l == 0) {
+    io.n_out[g] = k;
+    io.status[g] = st;
+  }
+}
+
 }  // namespace crdt
