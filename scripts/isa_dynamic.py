@@ -18,6 +18,7 @@ import re
 import sys
 
 SYM = "_ZN4crdt8k_replayILi32EEEvNS_5PoolsEjjjPKj"
+FILTER = int(os.environ.get("FILTER_CALL_LINE", "0"))  # only code inlined from a call at this line
 
 
 def load_dis(path):
@@ -254,6 +255,8 @@ def main():
         prev_cnt = cnt
         for (a, mn, _), (fl, ln, ch) in zip(blk, info):
             if mn.startswith(("s_nop", "s_waitcnt")):
+                continue
+            if FILTER and not any(d.call_line == FILTER for d in ch):
                 continue
             kind = ("branch" if mn.startswith(("s_cbranch", "s_branch")) else "scratch" if mn.startswith("scratch_")
                     else "salu" if mn.startswith("s_")

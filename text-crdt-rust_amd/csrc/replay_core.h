@@ -485,7 +485,9 @@ struct Replayer {
     }
     if (!tracked()) return false;  // (only remote ops look orders up: the host tracks their documents)
     u32 lf = w.ld(w.at(lof(), order));
-    if (lf == INVALID || lf == cl) return false;
+    // (the fast paths leave the entries of delete orders unwritten: any value may be read there,
+    // so a leaf id is trusted only if it exists, and then only if the order is found in it)
+    if (lf >= g(S_N_LEAVES) || lf == cl) return false;
     if (load) {
       ensure(lf);
       idx = w.cfind_order(g(C_N), order);
@@ -1403,7 +1405,7 @@ struct Replayer {
                        : Span{t1, ha ? t1 - 1u : e.ol, e.orr, -(i32)l};
         m -= can_append_u(last, w.cget(idx + 1u));
       }
-      if (n + m > (u32)L) return 0;  // a leaf split: the general path's job
+      if (n + m > (u32)L) return split_delete(idx, off, l, t1, first, per);  // the leaf must split
     }
     u32 k = 1, back = 0;
     u32 key = g(T_AGL_KEY);
@@ -1480,9 +1482,34 @@ struct Replayer {
     } else {
       append_delete(first, t1, done * l);  // forward deletes coalesce into one run (Rle::append)
     }
-    map_fill(first, done * l, INVALID);  // delete orders name no item
-    fast_txn_commit(first, done * l);
+    fast_txn_commit(first, done * l);  // (delete orders name no item: no order -> leaf entries)
     return done * per;
+  }
+  // One delete of l items at offset `off` of visible entry idx that needs a leaf split: exactly
+  // what apply_txn does for it -- mutate_entry (mutations.rs:227-277: the entry's first part stays,
+  // the deleted piece and the remainder are inserted after it) and insert_internal with its split
+  // (mutations.rs:17-179, split_at :623-669) -- then the fast txn bookkeeping.  Capacity as fits()
+  // for a one-op txn; 0 (nothing changed) sends the txn to the general path.
+  CRDT_HD u32 split_delete(u32 idx, u32 off, u32 l, u32 t1, u32 first, u32 per) {
+    if (g(K_LEAF) - g(S_N_LEAVES) < 2u) return 0;
+    if (g(K_DEL) == g(S_N_DEL)) return 0;
+    if (g(K_MAP) - first < l) return 0;
+    Span e = w.cget(idx);
+    u32 elen = slen(e);
+    u32 ha = off > 0u, hc = 0u;
+    Span pa{0, 0, 0, 0}, pc{0, 0, 0, 0};
+    if (ha) { elen -= off; pa = truncate_keeping_right(e, off); }
+    if (l < elen) { pc = truncate(e, l); hc = 1u; }
+    e.len = -e.len;
+    Span first_part = ha ? pa : e;
+    set(idx, first_part);
+    Cursor c{g(C_LEAF), idx, slen(first_part)};
+    Span a0 = ha ? e : pc;
+    u32 n = ha ? 1u + hc : hc;
+    insert_items(a0, pc, Span{0, 0, 0, 0}, n, c, g(C_LEAF));  // (n <= 2: cannot fail)
+    append_delete(first, t1, l);  // (delete orders name no item: no order -> leaf entries)
+    fast_txn_commit(first, l);
+    return per;
   }
   // Insert one item run right after the cursor (idx, off), 0 < off <= |entry|, when integrate
   // stops at once and the run cannot be appended: insert_internal (mutations.rs:17-179) splits
@@ -1605,6 +1632,14 @@ struct Replayer {
       }
       // no room for the item (+ the entry's remainder): a leaf split, the general path's job
       if (g(C_N) + 1u + (c.off < el) > (u32)L) {
+        // integrate stops at once here (checked above), so apply_txn would only insert_internal
+        // the item, splitting the leaf (mutations.rs:17-179): do that here when a leaf is free
+        if ((g(K_LEAF) - g(S_N_LEAVES) >= 2u) & (g(K_MAP) - first >= l)) {
+          insert_items(item, Span{0, 0, 0, 0}, Span{0, 0, 0, 0}, 1u, c, INVALID);
+          inc(S_N_ITEMS, l);
+          fast_txn_commit(first, l);
+          return per;
+        }
         pre = 1;
         pre_item = item;
         pre_c = c;
