@@ -1397,6 +1397,7 @@ struct Replayer {
   CRDT_HD u32 fast_deletes(u32 b0, u32 nv, u32 remote, u32 agent, u32 idx, u32 off, u32 l, u32 first, const Rec& o) {
     u32 per = per_txn(remote);
     u32 t1 = w.cget_order(idx) + off;
+    u32 split_first = 0;
     if (g(C_N) + 2u > (u32)L) {  // near-full leaf: does the first delete fit (leaf_delete's rule)?
       Span e = w.cget(idx);
       u32 n = g(C_N), ha = off > 0u, hc = off + l < (u32)e.len, m = ha + hc;
@@ -1405,7 +1406,7 @@ struct Replayer {
                        : Span{t1, ha ? t1 - 1u : e.ol, e.orr, -(i32)l};
         m -= can_append_u(last, w.cget(idx + 1u));
       }
-      if (n + m > (u32)L) return split_delete(idx, off, l, t1, first, per);  // the leaf must split
+      if (n + m > (u32)L) split_first = 1;  // the leaf must split for it
     }
     u32 k = 1, back = 0;
     u32 key = g(T_AGL_KEY);
@@ -1452,17 +1453,28 @@ struct Replayer {
 #endif
     if (g(K_MAP) - first < k * l) return 0;
     if (g(K_DEL) - g(S_N_DEL) < k) return 0;
-    u32 done = k >= 2u ? delete_run_closed(idx, off, t1, k, back) : 0u;
-    if (done == 0u) {  // op by op
-      for (u32 j = 0; j < k; j++) {
-        u32 ij = back ? idx : (j == 0u ? idx : idx + (off > 0u) + j);  // forward: the remainder moves right
-        u32 oj = back ? off - j : (j == 0u ? off : 0u);
-        u32 tj = back ? t1 - j : t1 + j;
-        if (w.cget_order(ij) + oj != tj) break;
-        if (w.cget_len(ij) <= (i32)oj) break;
-        if (!leaf_delete(ij, oj, l)) break;
-        done++;
+    u32 done = split_first ? 0u : delete_segment(idx, off, t1, k, back, l);
+    // The leaf ran out of room (or the run reached a shape the segment does not take): the next
+    // delete goes the general way -- mutate_entry + insert_internal, splitting the leaf -- and the
+    // rest of the run continues from wherever its next target now lives.
+    while (done < k) {
+      if (g(K_LEAF) - g(S_N_LEAVES) < 2u) break;
+      Cursor c{g(C_LEAF), idx, off};
+      if (done != 0u) {
+        if (!find_order(back ? t1 - done : t1 + done, true, c)) break;
       }
+      i32 el = w.cget_len(c.idx);
+      if (el <= 0) break;
+      if (c.off + l > (u32)el) break;
+      delete_general(c.idx, c.off, l);
+      done++;
+      if (done == k) break;
+      u32 t2 = back ? t1 - done : t1 + done;
+      if (!find_order(t2, true, c)) break;
+      el = w.cget_len(c.idx);
+      if (el <= 0) break;
+      if (c.off + l > (u32)el) break;
+      done += delete_segment(c.idx, c.off, t2, k - done, back, l);
     }
     if (done == 0u) return 0;
 #ifdef CRDT_PROF
@@ -1485,15 +1497,28 @@ struct Replayer {
     fast_txn_commit(first, done * l);  // (delete orders name no item: no order -> leaf entries)
     return done * per;
   }
-  // One delete of l items at offset `off` of visible entry idx that needs a leaf split: exactly
-  // what apply_txn does for it -- mutate_entry (mutations.rs:227-277: the entry's first part stays,
-  // the deleted piece and the remainder are inserted after it) and insert_internal with its split
-  // (mutations.rs:17-179, split_at :623-669) -- then the fast txn bookkeeping.  Capacity as fits()
-  // for a one-op txn; 0 (nothing changed) sends the txn to the general path.
-  CRDT_HD u32 split_delete(u32 idx, u32 off, u32 l, u32 t1, u32 first, u32 per) {
-    if (g(K_LEAF) - g(S_N_LEAVES) < 2u) return 0;
-    if (g(K_DEL) == g(S_N_DEL)) return 0;
-    if (g(K_MAP) - first < l) return 0;
+  // Up to k one-item deletes of a run (the first at `off` of entry idx, target t), in closed form
+  // or op by op, while the leaf has room.  Returns the deletes applied.
+  CRDT_HD u32 delete_segment(u32 idx, u32 off, u32 t, u32 k, u32 back, u32 l) {
+    u32 done = k >= 2u ? delete_run_closed(idx, off, t, k, back) : 0u;
+    if (done == 0u) {  // op by op
+      for (u32 j = 0; j < k; j++) {
+        u32 ij = back ? idx : (j == 0u ? idx : idx + (off > 0u) + j);  // forward: the remainder moves right
+        u32 oj = back ? off - j : (j == 0u ? off : 0u);
+        u32 tj = back ? t - j : t + j;
+        if (w.cget_order(ij) + oj != tj) break;
+        if (w.cget_len(ij) <= (i32)oj) break;
+        if (!leaf_delete(ij, oj, l)) break;
+        done++;
+      }
+    }
+    return done;
+  }
+  // One delete of l items at offset `off` of visible entry idx, exactly as apply_txn does it:
+  // mutate_entry (mutations.rs:227-277: the entry's first part stays, the deleted piece and the
+  // remainder are inserted after it) and insert_internal, splitting the leaf when it is full
+  // (mutations.rs:17-179, split_at :623-669).  The caller checked that a leaf is free.
+  CRDT_HD void delete_general(u32 idx, u32 off, u32 l) {
     Span e = w.cget(idx);
     u32 elen = slen(e);
     u32 ha = off > 0u, hc = 0u;
@@ -1507,9 +1532,6 @@ struct Replayer {
     Span a0 = ha ? e : pc;
     u32 n = ha ? 1u + hc : hc;
     insert_items(a0, pc, Span{0, 0, 0, 0}, n, c, g(C_LEAF));  // (n <= 2: cannot fail)
-    append_delete(first, t1, l);  // (delete orders name no item: no order -> leaf entries)
-    fast_txn_commit(first, l);
-    return per;
   }
   // Insert one item run right after the cursor (idx, off), 0 < off <= |entry|, when integrate
   // stops at once and the run cannot be appended: insert_internal (mutations.rs:17-179) splits
