@@ -72,6 +72,12 @@ enum : u32 {
   P_PROBE = P_DDB + 2,  // (2 slots) probe answers
   // 1: the txn-level invariants fast_txn_ok checks hold (set by a fast commit, cleared by apply_txn)
   F_FAST = P_PROBE + 2,
+  // a one-insert txn the fast path resolved but could not place (no free leaf for its split):
+  // flag, the item (4) and the cursor after its origin_left (3), handed to apply_txn.  Context
+  // lanes, not registers: this is the rare path, and registers live around the replay loop are
+  // what the 8-waves/SIMD budget spills.
+  F_PRE, PRE_ITEM, PRE_C = PRE_ITEM + 4,
+  F_GEN = PRE_C + 3,  // the record being replayed is a GEN record (generated ops)
   N_SLOTS
 };
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
@@ -81,11 +87,6 @@ static_assert(N_SLOTS <= 128, "two context registers");
 template <class W, int L>
 struct Replayer {
   W w;  // owned by value: its lane registers stay SSA values, never a scratch object
-  // A one-insert txn the fast path resolved but could not place (its leaf must split): the item
-  // and the cursor after its origin_left, handed to apply_txn so it skips the op's lookups.
-  u32 pre = 0;
-  Span pre_item{0, 0, 0, 0};
-  Cursor pre_c{0, 0, 0};
   // record format of the txn fast_txn is working on: compact one-record txns (RC / LC) or the
   // general header + ops (+ parents) form
   u32 cpt = 0;
@@ -187,6 +188,8 @@ struct Replayer {
     p(T_AGL_KEY, 0); p(T_AGL_ORDER, 0); p(T_AGL_LEN, 0);
     p(T_RB_BASE, 0x80000000u);  // pos - rb_base >= 64 for every valid pos
     p(F_FAST, 0);
+    p(F_PRE, 0);
+    p(F_GEN, 0);
   }
 
   CRDT_HD Span* leafp(u32 leaf) const { return w.template at<L>(lv(), leaf); }
@@ -1016,9 +1019,9 @@ struct Replayer {
     u32 remaining = 0, target = 0, lpos = 0, lins = 0;
     Span item{0, 0, 0, 0};
     Cursor c{0, 0, 0};
-    if (pre) {  // a fast-path attempt already resolved this one-insert txn (origins, cursor)
-      item = pre_item;
-      c = pre_c;
+    if (g(F_PRE)) {  // a fast-path attempt already resolved this one-insert txn (origins, cursor)
+      item = Span{g(PRE_ITEM), g(PRE_ITEM + 1), g(PRE_ITEM + 2), (i32)g(PRE_ITEM + 3)};
+      c = Cursor{g(PRE_C), g(PRE_C + 1), g(PRE_C + 2)};
       next = first + (u32)item.len;
       k = 1;
       mode = M_INS;
@@ -1662,9 +1665,9 @@ struct Replayer {
           fast_txn_commit(first, l);
           return per;
         }
-        pre = 1;
-        pre_item = item;
-        pre_c = c;
+        p(F_PRE, 1u);
+        p(PRE_ITEM, item.order); p(PRE_ITEM + 1, item.ol); p(PRE_ITEM + 2, item.orr); p(PRE_ITEM + 3, (u32)item.len);
+        p(PRE_C, c.leaf); p(PRE_C + 1, c.idx); p(PRE_C + 2, c.off);
         return 0;
       }
       // the typing that follows the inserted item appends to it: one entry for the whole run
@@ -1729,9 +1732,10 @@ struct Replayer {
       u32 gen = opq(kind == REC_GEN ? 1u : 0u);
       Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
       u32 inl = 0;
-      if (gen) {
+      if (gen) {  // (F_GEN carries the flag past the txn: no register lives across the loop body)
         u32 done = g(S_GEN_DONE);
-        if (done >= h.w2) { p(S_GEN_DONE, 0); pos += 1; continue; }
+        if (done >= h.w2) { p(S_GEN_DONE, 0); p(F_GEN, 0); pos += 1; continue; }
+        p(F_GEN, 1);
         gop = gen_op(h.w3, done, cur_len());
         h = Rec{(REC_LTXN << 28) | 1u, h.w1, gop.w2, gop.w2 + gop.w3};
         kind = REC_LTXN;
@@ -1759,7 +1763,7 @@ struct Replayer {
         else inc(S_PROF3, dt);
 #endif
         if (fast) {
-          if (gen) inc(S_GEN_DONE);
+          if (g(F_GEN)) inc(S_GEN_DONE);
           else pos += fast;
           continue;
         }
@@ -1769,7 +1773,7 @@ struct Replayer {
         u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
         consumed = inl ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, inl, gop, gpar) : ST_BAD_INPUT;
-        pre = 0;
+        p(F_PRE, 0u);
 #ifdef CRDT_PROF
         if (prof_mode != 3u) inc(S_PROF1, prof_mode == 0u ? (u32)(w.clock() - t1) : 1u);
 #endif
@@ -1783,7 +1787,7 @@ struct Replayer {
       }
       if (st == ST_NEED_CAPACITY) { p(S_STATUS, (u32)st); break; }  // resumable at `pos` after growth
       if (st != ST_OK) { p(S_STATUS, (u32)st); pos += consumed; break; }
-      if (gen) { inc(S_GEN_DONE); continue; }
+      if (g(F_GEN)) { inc(S_GEN_DONE); continue; }
       pos += consumed;
     }
     p(S_REC_POS, pos);
