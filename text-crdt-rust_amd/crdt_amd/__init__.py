@@ -43,11 +43,16 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defin
         if all(os.path.getmtime(s) <= lt for s in srcs):
             return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    # -phi-elim-split-all-critical-edges: the replay's fast paths have many early exits into one
-    # shared "not applicable" block; without edge splitting the register copies that block's phis
-    # need are placed before every conditional branch and run on the taken-or-not path alike.
+    # Codegen options for the replay's wave-uniform control flow (measured on k_replay, 8,192 AP
+    # documents, scripts/gpu_ab.sh):
+    #  -phi-elim-split-all-critical-edges: the fast paths have many early exits into one shared
+    #   "not applicable" block; without edge splitting the register copies that block's phis need
+    #   are placed before every conditional branch and run whether it is taken or not (118 -> 110 ms);
+    #  -structurizecfg-skip-uniform-regions: uniform branches stay plain s_cbranch_scc jumps instead
+    #   of being structurized into exec-mask flow blocks with 64-bit boolean phis (109 -> 99 ms).
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-fno-strict-aliasing", "-mllvm", "-phi-elim-split-all-critical-edges=1", "-I" + INCLUDE, "-I" + CSRC, "-o", out + ".tmp"] + ["-D" + d for d in defines] + [
+           "-fno-strict-aliasing", "-mllvm", "-phi-elim-split-all-critical-edges=1",
+           "-mllvm", "-structurizecfg-skip-uniform-regions=1", "-I" + INCLUDE, "-I" + CSRC, "-o", out + ".tmp"] + ["-D" + d for d in defines] + [
            os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "trace_ingest.cpp"), "-lz"]
     r = subprocess.run(cmd, capture_output=not verbose, text=True)
     if r.returncode != 0:
