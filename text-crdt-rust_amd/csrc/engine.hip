@@ -146,6 +146,7 @@ struct crdt_engine {
   Span* canon = nullptr;
   u32* vpos = nullptr;
   u32* sorted = nullptr;
+  u32* corder = nullptr;  // first order of every canonical span (k_pub_index input)
   u32* pub = nullptr;
   u64 canon_alloc = 0, pub_alloc = 0;
   bool pub_sized = false;   // the index pools fit the device state (else publish sizes them first)
@@ -153,6 +154,9 @@ struct crdt_engine {
   // publish launches: documents with >= PUB_BIG_MIN leaves get a workgroup each (k_publish_big)
   std::vector<u32> pub_small, pub_big;
   u32* pub_list = nullptr;  // [small docs..., big docs...] when there are big ones
+  // the small documents' order -> span index is built in LDS (k_pub_index) when their bitmap has
+  // at most PUBX_MAX_WORDS words; pubx_words = the largest such bitmap (the launch's LDS size)
+  u32 pubx_words = 0;
   u32* tlen = nullptr;
   u64* tdigest = nullptr;
   bool materialized = false;
@@ -188,6 +192,7 @@ struct crdt_engine {
     o.canon = canon;
     o.vpos = vpos;
     o.sorted = sorted;
+    o.corder = corder;
     o.pub = pub;
     o.canon_n = canon_n;
     o.len = len;
@@ -197,7 +202,7 @@ struct crdt_engine {
 
   void release() {
     pools.free_all();
-    dfree(canon); dfree(vpos); dfree(sorted); dfree(pub); dfree(pub_list);
+    dfree(canon); dfree(vpos); dfree(sorted); dfree(corder); dfree(pub); dfree(pub_list);
     pub_small.clear();
     pub_big.clear();
     canon_alloc = pub_alloc = 0;
@@ -368,11 +373,12 @@ struct crdt_engine {
       s.pub_base = npub; npub += 2ull * pub_words(s.ord_cap);
     }
     if (ncan > canon_alloc || ncan < canon_alloc / 2) {
-      dfree(canon); dfree(vpos); dfree(sorted);
+      dfree(canon); dfree(vpos); dfree(sorted); dfree(corder);
       canon_alloc = 0;
       HIPCHK(dalloc(canon, ncan));
       HIPCHK(dalloc(vpos, ncan));
       HIPCHK(dalloc(sorted, ncan));
+      HIPCHK(dalloc(corder, ncan));
       canon_alloc = ncan;
     }
     if (npub > pub_alloc || npub < pub_alloc / 2) {
@@ -388,10 +394,13 @@ struct crdt_engine {
     // thousands of mid-sized documents one wave each moves more per second)
     pub_small.clear();
     pub_big.clear();
+    pubx_words = 0;
     for (u64 d = 0; d < n_docs; d++) {
       u32 nl = st_h[d].n_leaves;
       bool big = nl >= PUB_BIG_MAX || (nl >= PUB_BIG_MIN && n_docs <= PUB_BIG_FEW_DOCS);
       (big ? pub_big : pub_small).push_back((u32)d);
+      u32 nw = pub_words(seg_h[d].ord_cap);
+      if (!big && nw <= PUBX_MAX_WORDS) pubx_words = std::max(pubx_words, nw);
     }
     dfree(pub_list);
     if (!pub_big.empty()) {
@@ -754,9 +763,16 @@ struct crdt_engine {
     u32 ns = pub_list ? (u32)pub_small.size() : (u32)n_docs;
     blocks = (ns + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     if (ns) {
-      if (L == 32) hipLaunchKernelGGL(k_publish<32>, dim3(blocks), dim3(256), 0, stream, pv, ov, ns, (const u32*)pub_list);
-      else hipLaunchKernelGGL(k_publish<4>, dim3(blocks), dim3(256), 0, stream, pv, ov, ns, (const u32*)pub_list);
+      // documents whose bitmap fits pubx_words get their index from k_pub_index (k_publish skips it)
+      u32 xw = pubx_words;
+      if (L == 32) hipLaunchKernelGGL(k_publish<32>, dim3(blocks), dim3(256), 0, stream, pv, ov, ns, (const u32*)pub_list, xw);
+      else hipLaunchKernelGGL(k_publish<4>, dim3(blocks), dim3(256), 0, stream, pv, ov, ns, (const u32*)pub_list, xw);
       HIPCHK(hipGetLastError());
+      if (xw) {
+        hipLaunchKernelGGL(k_pub_index, dim3(ns), dim3(PUBX_THREADS), pubx_lds_bytes(xw), stream, pv, ov,
+                           (const u32*)pub_list, xw);
+        HIPCHK(hipGetLastError());
+      }
     }
     if (pub_list && !pub_big.empty()) {
       const u32* bl = pub_list + pub_small.size();
@@ -921,6 +937,8 @@ int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
   // the replay's LDS root may take a workgroup's whole 160 KiB (one wave per workgroup)
   (void)hipFuncSetAttribute((const void*)k_replay<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_pub_index, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)pubx_lds_bytes(PUBX_MAX_WORDS));
   for (auto& x : e->ev)
     if (hipEventCreate(&x) != hipSuccess) return CRDT_E_DEVICE;
   *out = e.release();
@@ -1471,7 +1489,7 @@ int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23) {
 
 uint64_t crdt_mem_bytes(const crdt_engine* e) {
   if (!e) return 0;
-  return e->pools.bytes + e->rec_cap * sizeof(Rec) + e->content_cap * 4 + e->text_cap * 4 + e->canon_alloc * 24 +
+  return e->pools.bytes + e->rec_cap * sizeof(Rec) + e->content_cap * 4 + e->text_cap * 4 + e->canon_alloc * 28 +
          e->pub_alloc * 4 + e->probe_cap * 16 +
          e->n_docs * (sizeof(DocState) + sizeof(DocSeg) + 4 + 4 + 8);
 }

@@ -4,6 +4,7 @@
 //   k_relayout  move every document's state into re-sized pools (block per document)
 //   k_publish   flat index build: canonical spans (can_append compaction of the leaf entries in
 //               document order), visible-prefix vpos, order->span scatter, digest
+//   k_pub_index the order->span index of k_publish's documents, built in LDS (block per document)
 //   k_pos_to_loc / k_loc_to_pos   batched lookups on the published index (thread per query)
 //   k_materialize  document text from the published index + content streams (block per document)
 #pragma once
@@ -16,6 +17,8 @@ struct PubOut {
   Span* canon;    // [canon_base + k]
   u32* vpos;      // [canon_base + k]  visible items before canonical span k
   u32* sorted;    // [canon_base + r]  the canonical spans by first order (rank -> span)
+  u32* corder;    // [canon_base + k]  first order of canonical span k (k_pub_index's input: 4 B
+                  //                   per span instead of re-reading the 16 B spans)
   u32* pub;       // [pub_base + w]    bit (o & 31) of word o >> 5: a canonical span starts at order o;
                   // [pub_base + pub_words + w]  set bits in words [0, w)
   u32* canon_n;   // [doc]
@@ -203,6 +206,11 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
 #define PUB_BIG_FEW_DOCS 1024u   // ... when the batch has at most this many documents
 #define PUB_BIG_MAX 16384u       // leaves from which it always does
 
+// Digest term of canonical span k (section 1; oracle/crdt_oracle.hpp digest()).
+__device__ __forceinline__ u64 span_hash(u32 k, const Span& sp) {
+  return elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
+}
+
 // What one wave's leaf range contributes (k_publish_big boundary resolution).
 struct RangeSum {
   u32 spans;      // canonical spans starting in the range (its first entry counts as a start)
@@ -219,10 +227,13 @@ struct RangeSum {
 // registers).  WRITE: spans go to canon/vpos from index `out` with visible offsets from `vis`;
 // skip_first: the range's first span continues the previous range's (not written); extra: the
 // signed length the range's last span continues by in later ranges.  !WRITE: fill `sum`.
-template <int L, bool WRITE>
+// HASH: add every written span's digest term (elem_hash section 1) to h, lane-partial (k_publish:
+// the spans are hashed from registers as they are written, not re-read).  Every written span's
+// first order also goes to corder.
+template <int L, bool WRITE, bool HASH = false>
 __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg, u32 ng, u32 a, u32 b, Span* canon,
-                                              u32* vpos, u32 ccap, u32& out, u32& vis, u32 skip_first, i32 extra,
-                                              RangeSum& sum) {
+                                              u32* vpos, u32* corder, u32 ccap, u32& out, u32& vis, u32 skip_first,
+                                              i32 extra, RangeSum& sum, u64& h) {
   const u32 l = lane_id();
   const Span* leaves = P.leaves + seg.leaf_base * L;
   const GroupRec* groups = P.groups + seg.grp_base;  // the root level, read in order from HBM
@@ -303,7 +314,10 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
           if (WRITE) {
             if (skip) skip = 0;
             else {
-              if (l == 0u && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
+              if (l == 0u && out < ccap) {
+                canon[out] = open; vpos[out] = open_vpos; corder[out] = open.order;
+                if (HASH) h += span_hash(out, open);
+              }
               out++;
             }
           }
@@ -315,8 +329,11 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
         if (WRITE) {
           u32 sk = skip && firsts ? 1u : 0u;  // the skipped first span is the step's first start
           if (start && l != ls && rank >= sk && out + rank - sk < ccap) {
-            canon[out + rank - sk] = Span{v.x, v.y, v.z, glen};
+            Span sp{v.x, v.y, v.z, glen};
+            canon[out + rank - sk] = sp;
             vpos[out + rank - sk] = vis + V - cl;
+            corder[out + rank - sk] = v.x;
+            if (HASH) h += span_hash(out + rank - sk, sp);
           }
           out += firsts - sk;
           if (sk) skip = 0;
@@ -336,7 +353,10 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
     else sum.single = 0;
     if (WRITE && !skip) {
       open.len += extra;
-      if (l == 0 && out < ccap) { canon[out] = open; vpos[out] = open_vpos; }
+      if (l == 0 && out < ccap) {
+        canon[out] = open; vpos[out] = open_vpos; corder[out] = open.order;
+        if (HASH) h += span_hash(out, open);
+      }
       out++;
     }
   }
@@ -352,7 +372,7 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
 // Reads go through L2 (ld_l2): other lanes wrote them.  Wave `wv` of `nwv` takes every nwv-th
 // chunk; the word prefix is one contiguous word range per wave plus a cross-wave carry (lds_c:
 // nwv u32 of LDS, k_publish_big only).  Returns this wave's share of the canonical-span hash.
-template <int NWV>
+template <int NWV, bool HASH = true>
 __device__ __forceinline__ u64 publish_index(const PubOut& O, const DocSeg& seg, const DocState& s, const Span* canon,
                                              u32 out, u32 wv, u32* lds_c) {
   const u32 l = lane_id();
@@ -371,7 +391,7 @@ __device__ __forceinline__ u64 publish_index(const PubOut& O, const DocSeg& seg,
   for (u32 k0 = wv * 64u; k0 < out; k0 += 64u * NWV) {
     u32 k = k0 + l;
     Span sp = k < out ? canon[k] : Span{0, 0, 0, 0};
-    if (k < out) h += elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
+    if (HASH && k < out) h += span_hash(k, sp);
 #ifndef PUB_NO_INDEX
     // nearby spans share bitmap words: OR each distinct word's bits across the wave first, then
     // one atomic per word (same-address atomics serialise at L2)
@@ -483,8 +503,12 @@ __device__ __forceinline__ u64 digest_counts(const DocState& s, u32 out) {
   return counts ^ elem_hash(9, 0, ((u64)s.n_dd << 32) | s.n_txn, ((u64)s.n_fr << 32) | s.n_par);
 }
 
+// xw: documents whose bitmap has at most xw words get their order -> span index from k_pub_index
+// (launched next); the others build it here.
+// (8 waves per SIMD need <= 80 SGPRs: unconstrained, the compiler took 102, i.e. 6 waves per SIMD and
+// 8,192 documents in 1.33 rounds)
 template <int L>
-__global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n, const u32* list) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_publish(Pools P, PubOut O, u32 n, const u32* list, u32 xw) {
   u32 d;
   if (!wave_doc(WAVES_PER_BLOCK, list, n, d)) return;
   WaveGPU<L> w;
@@ -499,13 +523,15 @@ __global__ __launch_bounds__(256) void k_publish(Pools P, PubOut O, u32 n, const
   u32* vpos = O.vpos + seg.canon_base;
   u32 out = 0, vis = 0;
   RangeSum sum{};
-  compact_range<L, true>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, seg.canon_cap, out, vis, 0u, 0, sum);
+  u64 h = 0;
+  compact_range<L, true, true>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, O.corder + seg.canon_base, seg.canon_cap,
+                               out, vis, 0u, 0, sum, h);
   if (out > seg.canon_cap) {  // canonical spans beyond the planned capacity: report, never write past it
     if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  u64 h = publish_index<1>(O, seg, s, canon, out, 0u, nullptr);
+  if (pub_words(seg.ord_cap) > xw) h += publish_index<1, false>(O, seg, s, canon, out, 0u, nullptr);
   h += digest_tables<L>(P, seg, s, w);
   h = wave_sum64(h);
   if (l == 0) {
@@ -538,7 +564,9 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
   const u32 a = (u32)((u64)s.n_leaves * wv / NWV), b = (u32)((u64)s.n_leaves * (wv + 1u) / NWV);
   u32 out = 0, vis = 0;
   RangeSum sum{};
-  compact_range<L, false>(P, seg, s.ng, a, b, canon, vpos, seg.canon_cap, out, vis, 0u, 0, sum);
+  u64 h0 = 0;
+  u32* corder = O.corder + seg.canon_base;
+  compact_range<L, false>(P, seg, s.ng, a, b, canon, vpos, corder, seg.canon_cap, out, vis, 0u, 0, sum, h0);
   if (l == 0) s_sum[wv] = sum;
   __syncthreads();
   if (wv == 0) {  // boundary resolution, lane = range
@@ -563,7 +591,8 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
   out = s_base[wv];
   vis = s_vbase[wv];
   RangeSum sum2{};
-  compact_range<L, true>(P, seg, s.ng, a, b, canon, vpos, seg.canon_cap, out, vis, s_skip[wv], s_extra[wv], sum2);
+  compact_range<L, true>(P, seg, s.ng, a, b, canon, vpos, corder, seg.canon_cap, out, vis, s_skip[wv], s_extra[wv],
+                         sum2, h0);
   const u32 total = s_total;
   if (total > seg.canon_cap) {
     if (threadIdx.x == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
@@ -582,6 +611,77 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
     O.canon_n[d] = total;
     O.len[d] = s.len;
     O.digest[d] = mix64(t ^ digest_counts(s, total));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_pub_index: the order -> span index (publish_index's three sweeps) of the documents k_publish
+// left it to, one PUBX_THREADS block per document, with the bitmap in LDS: the bits are set with
+// LDS atomics (ds_or) instead of one global atomic per distinct word, and the word prefix and the
+// scatter's ranks read LDS instead of L2.  Global traffic per document: the span first orders
+// (corder, 4 B per span) twice, the bitmap and its word prefix written once, the rank -> span
+// table scattered once.  LDS: xw bitmap words + an exclusive prefix per 8-word group.
+// ---------------------------------------------------------------------------------------------
+#define PUBX_THREADS 256
+#define PUBX_MAX_WORDS 16384u  // bitmaps up to 524,288 orders (72 KiB of LDS: two blocks per CU)
+CRDT_HD inline u32 pubx_lds_bytes(u32 xw) { return (xw + xw / 8u + 1u) * 4u; }
+
+__global__ __launch_bounds__(PUBX_THREADS) void k_pub_index(Pools P, PubOut O, const u32* list, u32 xw) {
+  extern __shared__ u32 xl[];
+  __shared__ u32 s_w[PUBX_THREADS / 64];
+  u32* lb = xl;       // [xw] bitmap
+  u32* lg = xl + xw;  // [xw / 8 + 1] set bits in the 8-word groups before each group
+  const u32 d = list ? list[blockIdx.x] : blockIdx.x;
+  const u32 t = threadIdx.x;
+  const DocState* sp = P.st + d;
+  const DocSeg seg = P.seg[d];
+  const i32 status = sp->status;
+  const u32 next_order = sp->next_order;
+  if ((status != ST_OK && status != ST_NEED_CAPACITY) || next_order >= seg.ord_cap) return;
+  const u32 nw = pub_words(seg.ord_cap);
+  if (nw > xw) return;  // k_publish built this one
+  const u32 out = O.canon_n[d];  // 0 when k_publish refused the document
+  const u32 used = next_order / 32u + 1u;  // <= nw
+  const u32* co = O.corder + seg.canon_base;
+  u32* bits = O.pub + seg.pub_base;
+  u32* pre = bits + nw;
+  u32* sorted = O.sorted + seg.canon_base;
+  for (u32 i = t; i < used; i += PUBX_THREADS) lb[i] = 0u;
+  __syncthreads();
+  for (u32 k = t; k < out; k += PUBX_THREADS) {
+    u32 o = co[k];
+    atomicOr(lb + (o >> 5), 1u << (o & 31u));
+  }
+  __syncthreads();
+  // group prefix: thread t owns groups [g0, g1)
+  const u32 ngr = (used + 7u) / 8u, per = (ngr + PUBX_THREADS - 1u) / PUBX_THREADS;
+  const u32 g0 = t * per < ngr ? t * per : ngr, g1 = g0 + per < ngr ? g0 + per : ngr;
+  u32 c = 0;
+  for (u32 i = g0 * 8u; i < g1 * 8u && i < used; i++) c += (u32)__popc(lb[i]);
+  const u32 incl = wave_incl_scan(c);
+  if ((t & 63u) == 63u) s_w[t >> 6] = incl;
+  __syncthreads();
+  u32 run = incl - c;
+  for (u32 wv = 0; wv < (t >> 6); wv++) run += s_w[wv];
+  for (u32 g = g0; g < g1; g++) {
+    lg[g] = run;
+    for (u32 i = g * 8u; i < g * 8u + 8u && i < used; i++) run += (u32)__popc(lb[i]);
+  }
+  __syncthreads();
+  // the bitmap and its word prefix, written once (coalesced)
+  for (u32 i = t; i < used; i += PUBX_THREADS) {
+    u32 r = lg[i >> 3];
+    for (u32 j = i & ~7u; j < i; j++) r += (u32)__popc(lb[j]);
+    bits[i] = lb[i];
+    pre[i] = r;
+  }
+  // rank -> span
+  for (u32 k = t; k < out; k += PUBX_THREADS) {
+    u32 o = co[k], wd = o >> 5;
+    u32 r = lg[wd >> 3];
+    for (u32 j = wd & ~7u; j < wd; j++) r += (u32)__popc(lb[j]);
+    r += (u32)__popc(lb[wd] & ((1u << (o & 31u)) - 1u));
+    sorted[r] = k;
   }
 }
 
