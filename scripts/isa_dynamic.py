@@ -18,7 +18,8 @@ import re
 import sys
 
 SYM = "_ZN4crdt8k_replayILi32EEEvNS_5PoolsEjjjPKj"
-FILTER = int(os.environ.get("FILTER_CALL_LINE", "0"))  # only code inlined from a call at this line
+FILTER = int(os.environ.get("FILTER_CALL_LINE", "0"))
+MNS = tuple(x for x in os.environ.get("FILTER_MN", "").split(",") if x)  # only these mnemonic prefixes  # only code inlined from a call at this line
 
 
 def load_dis(path):
@@ -229,6 +230,7 @@ def main():
     if cur:
         blocks.append(cur)
     kinds = collections.Counter()
+    by_mn = collections.Counter()
     by_line = collections.defaultdict(collections.Counter)
     by_fn = collections.defaultdict(collections.Counter)
     prev_cnt = 0.0
@@ -258,16 +260,22 @@ def main():
                 continue
             if FILTER and not any(d.call_line == FILTER for d in ch):
                 continue
+            if MNS and not mn.startswith(MNS):
+                continue
             kind = ("branch" if mn.startswith(("s_cbranch", "s_branch")) else "scratch" if mn.startswith("scratch_")
                     else "salu" if mn.startswith("s_")
                     else "lane" if mn.startswith(("v_readlane", "v_writelane", "v_readfirstlane"))
                     else "valu" if mn.startswith("v_") else "mem")
             fn = ch[-1].name if ch else SYM
             kinds[kind] += cnt
+            by_mn[mn] += cnt
             by_line[(fl, ln)][kind] += cnt
             by_fn[fn][kind] += cnt
     tot = sum(kinds.values())
     print(f"estimated per op: total {tot / ops:.1f}  " + "  ".join(f"{k} {v / ops:.1f}" for k, v in kinds.items()))
+    print("\nby mnemonic, per op:")
+    for mn, c in by_mn.most_common(top):
+        print(f"  {c / ops:7.2f}  {mn}")
     print("\nby function (innermost inlined instance), per op:")
     for fn, c in sorted(by_fn.items(), key=lambda kv: -sum(kv[1].values()))[:top]:
         print(f"  {sum(c.values()) / ops:7.2f}  salu {c['salu'] / ops:6.2f}  valu {c['valu'] / ops:6.2f}  lane {c['lane'] / ops:5.2f}  br {c['branch'] / ops:5.2f}  {fn[:90]}")
