@@ -119,6 +119,8 @@ struct WaveCPU {
     return false;
   }
   i32 cfind_order(u32 n, u32 order) const {
+    // WaveGPU::cfind_order relies on it: the cached leaf's lanes from n on are empty
+    for (u32 i = n; i < 64; i++) if (c[i].len != 0) __builtin_trap();
     for (u32 i = 0; i < n; i++) if (order >= c[i].order && order - c[i].order < slen(c[i])) return (i32)i;
     return -1;
   }

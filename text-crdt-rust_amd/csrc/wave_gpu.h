@@ -23,6 +23,9 @@ __device__ __forceinline__ u32 lane_here() {
 }
 __device__ __forceinline__ u32 uni(u32 x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ u32 rdlane(u32 x, u32 l) { return __builtin_amdgcn_readlane(x, l); }
+// llvm.amdgcn.writelane (clang has no builtin for it): lane l of old := v (v, l uniform)
+__device__ int crdt_writelane_i32(int v, int l, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ u32 wrlane(u32 old, u32 v, u32 l) { return (u32)crdt_writelane_i32((int)v, (int)l, (int)old); }
 // (the builtin takes the i1 predicate directly: no v_cndmask + v_cmp round trip as __ballot has)
 __device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ u32 shfl(u32 v, u32 src) { return __builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
@@ -51,6 +54,16 @@ __device__ __forceinline__ u32 wave_or(u32 v) {
 
 template <int L>
 struct WaveGPU {
+  // The lane id, computed once; lane() hands out a copy at every use (volatile: never hoisted).  A
+  // hoisted lane id lets the compiler hoist every lane-derived constant (l | 32, l - 1, l * 16 ...)
+  // out of the replay loop, where each then holds a VGPR for the whole kernel and the
+  // 8-waves/SIMD register budget spills them.  One v_mov per use (two v_mbcnt re-deriving it).
+  u32 lid_ = lane_id();
+  __device__ __forceinline__ u32 lane() const {
+    u32 l;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "v"(lid_));
+    return l;
+  }
   // ---------------------------------------------------------------- context registers
   // Per-document scalar state, one field per lane (replay_core.h slot enum), accessed at
   // compile-time lane numbers: v_readlane / v_writelane, no memory, no SGPR pressure.
@@ -83,14 +96,14 @@ struct WaveGPU {
   }
   // DocState <-> slots [base, base + 20) of x0: one lane-parallel load / store
   __device__ __forceinline__ void x_load_state(const DocState* p, u32 base) {
-    u32 l = lane_here();
+    u32 l = lane();
     const u32* q = (const u32*)p;
     bool mine = l >= base && l < base + (u32)(sizeof(DocState) / 4);
     u32 v = q[mine ? l - base : 0u];  // clamped address: unconditional load, no exec branch
     x0 = mine ? v : x0;
   }
   __device__ __forceinline__ void x_store_state(DocState* p, u32 base) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32* q = (u32*)p;
     if (l >= base && l < base + (u32)(sizeof(DocState) / 4)) q[l - base] = x0;
   }
@@ -152,10 +165,16 @@ struct WaveGPU {
   // lane-parallel fill of n u32
   __device__ __forceinline__ void fill(u32* p, u32 n, u32 v) const {
     if (n == 1) { *p = v; return; }  // the common single-item case: one coalesced store
-    for (u32 k = lane_here(); k < n; k += 64) p[k] = v;
+    u32 l = lane();
+    if (n <= 64u) {  // one store, lanes >= n repeating item n - 1 (same value): no exec mask
+      u32 m = n - 1u;
+      p[l < m ? l : m] = v;
+      return;
+    }
+    for (u32 k = l; k < n; k += 64) p[k] = v;
   }
   __device__ __forceinline__ void zero_leaf(Span* p, u32 n) const {
-    u32 l = lane_here();
+    u32 l = lane();
     if (l < n) *(uint4*)(p + l) = make_uint4(0, 0, 0, 0);
   }
 
@@ -164,7 +183,7 @@ struct WaveGPU {
   __device__ __forceinline__ i32 search(const T* base, u32 n, u32 needle) const {
     if (n == 0) return -1;
     u32 lo = 0, hi = n;  // answer (last key <= needle) in [lo, hi)
-    u32 l = lane_here();
+    u32 l = lane();
     while (hi - lo > 64) {
       u32 step = (hi - lo + 63) / 64;
       u32 idx = lo + l * step;
@@ -200,7 +219,7 @@ struct WaveGPU {
   // last block with first key <= x, or -1 (64-ary search, as `search`)
   __device__ __forceinline__ i32 search_first(const DDBlk* b, u32 n, u32 x) const {
     u32 lo = 0, hi = n;
-    u32 l = lane_here();
+    u32 l = lane();
     while (hi - lo > 64) {
       u32 step = (hi - lo + 63) / 64;
       u32 idx = lo + l * step;
@@ -218,13 +237,13 @@ struct WaveGPU {
   }
   // entries of one block (cnt >= 1) with key <= x
   __device__ __forceinline__ u32 dd_count_le(const DDRun* blk, u32 cnt, u32 x) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 key = blk[l < cnt ? l : 0u].key;
     return (u32)__popcll(ballot(l < cnt && key <= x));
   }
   // entries [32, 64) of a full block move to [0, 32) of dst; returns dst's first key
   __device__ __forceinline__ u32 dd_split(const DDRun* src, DDRun* dst) const {
-    u32 l = lane_here();
+    u32 l = lane();
     const u32* s = (const u32*)(src + (l | 32u));
     u32 a = s[0], b = s[1], c = s[2];
     if (l >= 32u) {
@@ -235,7 +254,7 @@ struct WaveGPU {
   }
   // Vec::insert at i of a block with cnt < 64 entries: [i, cnt) move up one, r goes to i
   __device__ __forceinline__ void dd_block_insert(DDRun* blk, u32 cnt, u32 i, const DDRun& r) const {
-    u32 l = lane_here();
+    u32 l = lane();
     const u32* s = (const u32*)(blk + (l ? l - 1u : 0u));
     u32 a = s[0], b = s[1], c = s[2];
     bool me = l == i;
@@ -247,7 +266,7 @@ struct WaveGPU {
   // directory insert at `at` of n blocks: [at, n) move up one (64-block chunks, top down: each
   // chunk's loads complete before its stores, and no later chunk reads what it stores)
   __device__ __forceinline__ void ddb_insert(DDBlk* b, u32 n, u32 at, const DDBlk& v) const {
-    u32 l = lane_here();
+    u32 l = lane();
     for (i32 r = (i32)(n & ~63u); r >= (i32)(at & ~63u); r -= 64) {
       u32 i = (u32)r + l;
       uint4 x = *(const uint4*)(b + (i > 0u && i <= n ? i - 1u : 0u));
@@ -259,14 +278,14 @@ struct WaveGPU {
 
   // ---------------------------------------------------------------- leaf cache
   __device__ __forceinline__ u32 cache_load(const Span* p) {
-    u32 l = lane_here();
+    u32 l = lane();
     bool in = l < (u32)L;
     uint4 v = *(const uint4*)(p + (l & (u32)(L - 1)));  // lanes >= L re-read a valid entry
     eo = in ? v.x : 0u; el = in ? v.y : 0u; er = in ? v.z : 0u; en = in ? (i32)v.w : 0;
     return __popcll(ballot(en != 0));
   }
   __device__ __forceinline__ void cache_store(Span* p) const {
-    u32 l = lane_here();
+    u32 l = lane();
     if (l < (u32)L) *(uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
   }
   __device__ __forceinline__ Span cget(u32 i) const {
@@ -274,16 +293,17 @@ struct WaveGPU {
   }
   __device__ __forceinline__ u32 cget_order(u32 i) const { return rdlane(eo, i); }
   __device__ __forceinline__ i32 cget_len(u32 i) const { return (i32)rdlane((u32)en, i); }
-  __device__ __forceinline__ void cset(u32 i, const Span& s) {  // branch-free: 4 v_cndmask
-    bool me = lane_here() == i;
-    eo = me ? s.order : eo;
-    el = me ? s.ol : el;
-    er = me ? s.orr : er;
-    en = me ? s.len : en;
+  // entry i := s (i and s uniform): one v_writelane per field (the compiler sets M0 for a run-time
+  // lane select), instead of a lane-compare mask, an SGPR -> VGPR copy and a v_cndmask per field
+  __device__ __forceinline__ void cset(u32 i, const Span& s) {
+    eo = wrlane(eo, s.order, i);
+    el = wrlane(el, s.ol, i);
+    er = wrlane(er, s.orr, i);
+    en = (i32)wrlane((u32)en, (u32)s.len, i);
   }
   // entries [a, b) := f(lane), lane-parallel (f computes each lane's entry in VALU)
   template <class F> __device__ __forceinline__ void cset_lanes(u32 a, u32 b, F f) {
-    u32 l = lane_here();
+    u32 l = lane();
     Span s = f(l);
     bool in = l >= a && l < b;
     eo = in ? s.order : eo;
@@ -292,16 +312,18 @@ struct WaveGPU {
     en = in ? s.len : en;
   }
   // lanes [a, b) as a mask, and the lowest lane of a mask (wave-uniform)
-  __device__ __forceinline__ u64 lanes_in(u32 a, u32 b) const { u32 l = lane_here(); return ballot(l >= a && l < b); }
+  __device__ __forceinline__ u64 lanes_in(u32 a, u32 b) const { u32 l = lane(); return ballot(l >= a && l < b); }
   __device__ __forceinline__ static u32 first_lane(u64 m) { return (u32)__builtin_ctzll(m); }
   // leaf.rs:41-57 find on a leaf that is NOT the cached one (peek: no cache change)
   __device__ __forceinline__ i32 peek_find_order(const Span* p, u32 order, u32& start) const {
-    u32 l = lane_here();
+    u32 l = lane();
     uint4 v = *(const uint4*)(p + (l & (u32)(L - 1)));
     u32 o = v.x;
     i32 n = (i32)v.w;
     u32 sl = (u32)(n < 0 ? -n : n);
-    u64 m = ballot(l < (u32)L && n != 0 && order >= o && order - o < sl);
+    // one unsigned compare: order < o wraps to >= 2^31 > sl (orders < 2^31); empty entries have
+    // sl = 0; lanes >= L repeat lanes l & (L - 1), so the lowest match is < L
+    u64 m = ballot(order - o < sl);
     if (!m) return -1;
     u32 k = (u32)__builtin_ctzll(m);
     start = rdlane(o, k);
@@ -309,35 +331,40 @@ struct WaveGPU {
   }
   __device__ __forceinline__ u32 clen_l() const { return en > 0 ? (u32)en : 0u; }
   __device__ __forceinline__ u32 cache_vis_from(u32 a) const {  // visible items in lanes >= a
-    return wave_sum(lane_here() >= a ? clen_l() : 0u);
+    return wave_sum(lane() >= a ? clen_l() : 0u);
   }
   // leaf.rs:61-84 find_offset (stick_end = false) over clen
   __device__ __forceinline__ bool cfind_content(u32 n, u32 rem, u32& idx, u32& off) const {
-    u32 l = lane_here();
-    u32 x = l < n ? clen_l() : 0u;
+    u32 l = lane();
+    // lanes >= n are empty (clen 0: every cache update keeps the tail clear), so they add nothing
+    // and their prefix is the total: counted only when rem >= total, i.e. when k >= n anyway
+    (void)l;
+    u32 x = clen_l();
     u32 incl = wave_incl_scan(x);
-    u32 k = __popcll(ballot(l < n && incl <= rem));
+    u32 k = __popcll(ballot(incl <= rem));
     if (k < n) {
       idx = k;
       off = rem - (rdlane(incl, k) - rdlane(x, k));
       return true;
     }
-    u32 total = n ? rdlane(incl, n - 1) : 0u;
+    u32 total = rdlane(incl, 63);
     if (rem == total) { idx = n; off = 0; return true; }
     return false;
   }
   // leaf.rs:41-57 find
   __device__ __forceinline__ i32 cfind_order(u32 n, u32 order) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 sl = (u32)(en < 0 ? -en : en);
-    u64 m = ballot(l < n && order >= eo && order - eo < sl);
+    // one unsigned compare (order < eo wraps past sl; lanes >= n are empty: sl = 0)
+    (void)l; (void)n;
+    u64 m = ballot(order - eo < sl);
     return m ? (i32)(__builtin_ctzll(m)) : -1;
   }
   // the split-off entries [idx, n) of the cached leaf, after `padding` empty slots: written to
   // the new leaf and kept in registers (cache_from_moved) for a cursor that follows them
   u32 mo = 0, ml = 0, mr = 0, mn = 0;
   __device__ __forceinline__ void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 src = l + idx - padding;  // valid only when l >= padding
     u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
     bool take = l >= padding && src < n && l < (u32)L;
@@ -348,7 +375,7 @@ struct WaveGPU {
   // lof[order + t] = v for every item of the entries in lanes [a, b): 64 items per step, each
   // lane finding its entry by a 6-step search over the entries' length prefix
   __device__ __forceinline__ void fill_runs(u32* base, u32 a, u32 b, u32 v) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 ln = l >= a && l < b ? (u32)(en < 0 ? -en : en) : 0u;
     u32 Pi = wave_incl_scan(ln);
     u32 T = rdlane(Pi, 63);
@@ -362,32 +389,36 @@ struct WaveGPU {
     }
   }
   __device__ __forceinline__ void cache_clear(u32 a, u32 b) {
-    u32 l = lane_here();
+    u32 l = lane();
     bool z = l >= a && l < b;
     eo = z ? 0u : eo;
     el = z ? 0u : el;
     er = z ? 0u : er;
     en = z ? 0 : en;
   }
-  // entries [idx, n) move to [idx+k, n+k); the vacated slots [idx, idx+k) become empty
+  // entries [idx, n) move to [idx+k, n+k); the vacated slots [idx, idx+k) become empty.  Lanes
+  // >= idx take lane l - k, the gap's lanes take lane 63 (always empty: L <= 32), and lanes
+  // >= n + k take an empty lane >= n: no lane-range masks to combine.
   __device__ __forceinline__ void cache_shift_right(u32 idx, u32 n, u32 k) {
-    u32 l = lane_here();
-    u32 src = l - k;
+    static_assert(L <= 32, "lane 63 of the cache is always empty");
+    u32 l = lane();
+    (void)n;
+    u32 src = l >= idx + k ? l - k : 63u;
     u32 o = shfl(eo, src), a = shfl(el, src), b = shfl(er, src), c = shfl((u32)en, src);
-    bool mv = l >= idx + k && l < n + k;
-    bool z = l >= idx && l < idx + k;
-    eo = mv ? o : (z ? 0u : eo);
-    el = mv ? a : (z ? 0u : el);
-    er = mv ? b : (z ? 0u : er);
-    en = mv ? (i32)c : (z ? 0 : en);
+    bool up = l >= idx;
+    eo = up ? o : eo;
+    el = up ? a : el;
+    er = up ? b : er;
+    en = up ? (i32)c : en;
   }
 
   // ---------------------------------------------------------------- record window (64 + 64 ahead)
   u32 rx = 0, ry = 0, rz = 0, rw = 0;  // window: lane k = record base + k
   u32 qx = 0, qy = 0, qz = 0, qw = 0;  // next 64 records, loaded ahead
-  __device__ __forceinline__ static uint4 rec_lane_load(const Rec* p, u32 n) {  // n >= 1
-    u32 l = lane_here();
-    return *(const uint4*)(p + (l < n ? l : n - 1));
+  __device__ __forceinline__ uint4 rec_lane_load(const Rec* p, u32 n) const {  // n >= 1
+    u32 l = lane();
+    u32 m = n - 1u;
+    return *(const uint4*)(p + (l < m ? l : m));
   }
   __device__ __forceinline__ void rec_load2(const Rec* p, u32 n, u32 n_ahead) {
     uint4 v = rec_lane_load(p, n);
@@ -405,7 +436,7 @@ struct WaveGPU {
       d -= 64u;
     }
     if (d) {
-      u32 l = lane_here();
+      u32 l = lane();
       u32 src = (l + d) & 63u;
       bool own = l + d < 64u;
       u32 ax = shfl(rx, src), ay = shfl(ry, src), az = shfl(rz, src), aw = shfl(rw, src);
@@ -427,18 +458,22 @@ struct WaveGPU {
   // The txn at b0 was checked by the caller.  Returns the run length in txns (>= 1) and the
   // total inserted length.  nv = valid records in the block.
   // compact: one record per txn (crdt_types.h RC / LC), lane k checks record k against record k-1.
-  __device__ __forceinline__ static u32 typing_scan_r(u32 X, u32 Y, u32 Z, u32 Q, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3,
-                                             u32& total) {
-    u32 l = lane_here();
+  __device__ __forceinline__ u32 typing_scan_r(u32 X, u32 Y, u32 Z, u32 Q, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3,
+                                             u32& total) const {
+    u32 l = lane();
     if (compact) {
       u32 p0 = shfl(X, l - 1u), p1 = shfl(Y, l - 1u), p3 = shfl(Q, l - 1u);
       bool ok;
       u32 hl;
       if (remote) {
         hl = (X >> 16) & 0x7FFu;
-        u32 ra = Q == 0xFFFFFFFFu ? 0xFFFFu : agent;  // origin_right's agent (ROOT or the author)
-        ok = (X & RC_HDR_MASK) == ((REC_RC << 28) | agent) && hl != 0u && Y == p1 + ((p0 >> 16) & 0x7FFu) &&
-             Z == Y - 1u && Q == ow3 && (agent | (ra << 16)) == ow1;
+        // origin_right's agent (ROOT or the author) follows from Q == ow3: a uniform check
+        u32 ra = ow3 == 0xFFFFFFFFu ? 0xFFFFu : agent;
+        u32 ubad = (agent | (ra << 16)) != ow1 ? 1u : 0u;
+        // the equality terms folded into one word (one compare instead of a mask AND per term)
+        u32 d = ((X & RC_HDR_MASK) ^ ((REC_RC << 28) | agent)) | (Y ^ (p1 + ((p0 >> 16) & 0x7FFu))) |
+                (Z ^ (Y - 1u)) | (Q ^ ow3) | ubad;
+        ok = d == 0u && hl != 0u;
       } else {
         hl = Q;
         ok = X == ((REC_LC << 28) | agent) && Z == 0u && Q - 1u < 0xFFFFu && Y == p1 + p3;
@@ -478,12 +513,14 @@ struct WaveGPU {
   // seq + 1, RDEL of 1 item of `agent` at the previous target seq + delta, RPARENT (agent, seq-1);
   // local: LTXN{1 op} deleting 1 item at the previous pos + delta.  Returns the run length in
   // txns (>= 1; the txn at b0 was checked by the caller).
-  __device__ __forceinline__ static u32 delete_scan_r(u32 X, u32 Y, u32 Z, u32 Q, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) {
-    u32 l = lane_here();
+  __device__ __forceinline__ u32 delete_scan_r(u32 X, u32 Y, u32 Z, u32 Q, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+    u32 l = lane();
     if (compact) {  // one record per txn: lane k against record k-1
       u32 p1 = shfl(Y, l - 1u), p2 = shfl(Z, l - 1u);
-      bool ok = remote ? ((X == ((REC_RC << 28) | (1u << 27) | (1u << 16) | agent)) && Y == p1 + 1u && Z == p2 + delta)
-                       : (X == ((REC_LC << 28) | agent) && Z == 1u && Q == 0u && Y == p1 + delta);
+      // the equality terms folded into one word (one compare instead of a mask AND per term)
+      u32 d = remote ? ((X ^ ((REC_RC << 28) | (1u << 27) | (1u << 16) | agent)) | (Y ^ (p1 + 1u)) | (Z ^ (p2 + delta)))
+                     : ((X ^ ((REC_LC << 28) | agent)) | (Z ^ 1u) | Q | (Y ^ (p1 + delta)));
+      bool ok = d == 0u;
       u64 stop = ballot(l > b0 && (!ok || l >= nv));
       u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
       return f - b0;
@@ -530,7 +567,7 @@ struct WaveGPU {
   }
   // runs {key0 + j, t0 - j, 1} for j < cnt (backspaced deletes), lane-parallel
   __device__ __forceinline__ void st_del_run(DelRun* p, u32 cnt, u32 key0, u32 t0) const {
-    for (u32 j = lane_here(); j < cnt; j += 64) {
+    for (u32 j = lane(); j < cnt; j += 64) {
       u32* q = (u32*)(p + j);
       q[0] = key0 + j;
       q[1] = t0 - j;
@@ -544,13 +581,21 @@ struct WaveGPU {
   __device__ __forceinline__ lds_u32* rblk() const { return rt; }
   __device__ __forceinline__ lds_u32* rcnt() const { return rt + rcap; }
   __device__ __forceinline__ lds_u32* rvis() const { return rt + 2 * rcap; }
+  // Groups [ng, rcap) hold block id INVALID (no block has that id), so root_find_blk needs no
+  // bounds test; the root only grows while a wave runs (root_insert writes at most up to ng).
+  __device__ __forceinline__ void root_clear_from(u32 ng) {
+    for (u32 i = lane(); i < rcap; i += 64)
+      if (i >= ng) rblk()[i] = INVALID;
+  }
   __device__ __forceinline__ void root_init(u32 blk, u32 cnt, u32 vis) {
+    root_clear_from(1u);
     rblk()[0] = blk;  // every lane stores the same value: no branch
     rcnt()[0] = cnt;
     rvis()[0] = vis;
   }
   __device__ __forceinline__ void root_load(const GroupRec* g, u32 ng) {
-    for (u32 i = lane_here(); i < ng; i += 64) {
+    root_clear_from(ng);
+    for (u32 i = lane(); i < ng; i += 64) {
       uint4 x = *(const uint4*)(g + i);
       rblk()[i] = x.x;
       rcnt()[i] = x.y;
@@ -558,17 +603,17 @@ struct WaveGPU {
     }
   }
   __device__ __forceinline__ void root_store(GroupRec* g, u32 ng) const {
-    for (u32 i = lane_here(); i < ng; i += 64) *(uint4*)(g + i) = make_uint4(rblk()[i], rcnt()[i], rvis()[i], 0);
+    for (u32 i = lane(); i < ng; i += 64) *(uint4*)(g + i) = make_uint4(rblk()[i], rcnt()[i], rvis()[i], 0);
   }
   __device__ __forceinline__ u32 root_blk(u32 g) const { return uni(rblk()[g]); }
   __device__ __forceinline__ u32 root_cnt(u32 g) const { return uni(rcnt()[g]); }
   __device__ __forceinline__ u32 root_vis(u32 g) const { return uni(rvis()[g]); }
   __device__ __forceinline__ u32 root_find_blk(u32 ng, u32 blk) const {
-    u32 l = lane_here();
+    u32 l = lane();
     for (u32 r = 0; r < ng; r += 64) {
       u32 i = r + l;
       u32 b = rblk()[i];  // i < rcap (a multiple of 64): always inside this wave's LDS slice
-      u64 m = ballot(i < ng && b == blk);
+      u64 m = ballot(b == blk);  // (groups >= ng hold INVALID: root_clear_from)
       if (m) return r + (u32)__builtin_ctzll(m);
     }
     return INVALID;
@@ -586,7 +631,7 @@ struct WaveGPU {
   // read completely before it is written (a chunk's lane 0 reads the top of the chunk below,
   // which is written only afterwards)
   __device__ __forceinline__ void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
-    u32 l = lane_here();
+    u32 l = lane();
     for (i32 r = (i32)(ng & ~63u); r >= (i32)(g & ~63u); r -= 64) {
       u32 i = (u32)r + l;
       u32 jj = i > 0u ? i - 1u : 0u;
@@ -599,7 +644,7 @@ struct WaveGPU {
   }
   // first group whose cumulative visible count exceeds pos
   __device__ __forceinline__ bool root_find_pos(u32 ng, u32 pos, u32& g, u32& base) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 carry = 0;
     for (u32 r = 0; r < ng; r += 64) {
       u32 i = r + l;
@@ -608,7 +653,7 @@ struct WaveGPU {
       u32 x = valid ? xv : 0u;
       u32 incl = wave_incl_scan(x) + carry;
       u32 nvalid = ng - r < 64 ? ng - r : 64;
-      u32 k = __popcll(ballot(valid && incl <= pos));
+      u32 k = __popcll(ballot(incl <= pos));  // (invalid lanes add 0: counted only if k >= nvalid)
       if (k < nvalid) {
         g = r + k;
         base = rdlane(incl, k) - rdlane(x, k);
@@ -621,7 +666,7 @@ struct WaveGPU {
 
   // visible items in the groups before g (probe: Cursor::count_pos)
   __device__ __forceinline__ u32 root_vis_before(u32 g) const {
-    u32 l = lane_here(), t = 0;
+    u32 l = lane(), t = 0;
     for (u32 r = 0; r < g; r += 64) t += wave_sum(r + l < g ? (u32)rvis()[r + l] : 0u);
     return t;
   }
@@ -629,14 +674,14 @@ struct WaveGPU {
   // ---------------------------------------------------------------- directory blocks (HBM)
   // visible items in the slots before i of a block row
   __device__ __forceinline__ u32 blk_vis_before(const u32* dv, u32 i) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 x = dv[l];  // 64-slot rows: always in bounds
     return wave_sum(l < i ? x : 0u);
   }
   // visible items before entry idx of the cached leaf / of another leaf (+ that entry's length)
-  __device__ __forceinline__ u32 cache_vis_before(u32 idx) const { return wave_sum(lane_here() < idx ? clen_l() : 0u); }
+  __device__ __forceinline__ u32 cache_vis_before(u32 idx) const { return wave_sum(lane() < idx ? clen_l() : 0u); }
   __device__ __forceinline__ u32 peek_vis_before(const Span* p, u32 idx, i32& len_idx) const {
-    u32 l = lane_here();
+    u32 l = lane();
     i32 n = (i32)p[l & (u32)(L - 1)].len;
     len_idx = (i32)rdlane((u32)n, idx);
     return wave_sum(l < idx && l < (u32)L && n > 0 ? (u32)n : 0u);
@@ -647,11 +692,11 @@ struct WaveGPU {
   // slot of a block whose cumulative visible count first exceeds rem (+ its leaf id; both block
   // rows are loaded together so the descent costs one HBM round trip)
   __device__ __forceinline__ bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 xv = dv[l], lf = dl[l];  // block rows are 64 slots wide: always in bounds
     u32 x = l < cnt ? xv : 0u;
     u32 incl = wave_incl_scan(x);
-    u32 k = __popcll(ballot(l < cnt && incl <= rem));
+    u32 k = __popcll(ballot(incl <= rem));  // (lanes >= cnt add 0: counted only if k >= cnt)
     if (k >= cnt) return false;
     i = k;
     before = rdlane(incl, k) - rdlane(x, k);
@@ -659,7 +704,7 @@ struct WaveGPU {
     return true;
   }
   __device__ __forceinline__ void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 ol = *(u32*)(dl + l);
     u32 ov = *(u32*)(dv + l);
     u32 sl = shfl(ol, l - 1), sv = shfl(ov, l - 1);
@@ -672,7 +717,7 @@ struct WaveGPU {
     }
   }
   __device__ __forceinline__ u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
-    u32 l = lane_here();
+    u32 l = lane();
     u32 lf = 0, v = 0;
     if (l >= 32) {
       lf = *(const u32*)(dl + l);
