@@ -1362,7 +1362,8 @@ struct Replayer {
         u32 q = delta - (lane - idx - 1u);           // F_q
         u32 jc = p0 ? 2u * q : 2u * q - 1u;          // the op (1-based) that created it
         u32 tc = t1 - (jc - 1u);
-        return jc + 1u <= k ? Span{tc - 1u, tc - 1u, orr, -2} : Span{tc, tc - 1u, orr, -1};
+        u32 two = jc + 1u <= k ? 1u : 0u;  // {tc-1, tc-1, orr, -2} or {tc, tc-1, orr, -1}: arithmetic, no selects
+        return Span{tc - two, tc - 1u, orr, (i32)~two};
       });
       if (p0) w.cset(idx + 1u + delta, Span{t1, N0.ol, N0.orr, N0.len - 1});
       E.len = (i32)(off + 1u - k);
@@ -1729,6 +1730,21 @@ struct Replayer {
     while (pos < rn) {
       Rec h = rec(pos);
       u32 kind = rec_kind(h);
+      u32 tried = 0;  // the fast path already declined this record
+      if (kind == REC_RC) {
+        // the remote-batch hot loop: compact remote txns through one fast-path instance, in a loop
+        // of their own (its registers do not meet the other record kinds' paths at every txn)
+        u32 fast;
+        while ((fast = fast_txn(pos, REC_RC, 0u, h, Rec{0, 0, 0, 0})) != 0u) {
+          pos += fast;
+          if (pos >= rn) break;
+          h = rec(pos);
+          kind = rec_kind(h);
+          if (kind != REC_RC) break;
+        }
+        if (pos >= rn) break;
+        tried = kind == REC_RC ? 1u : 0u;
+      }
       u32 gen = opq(kind == REC_GEN ? 1u : 0u);
       Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
       u32 inl = 0;
@@ -1750,7 +1766,7 @@ struct Replayer {
         // compact remote txns (the remote-batch hot path) get their own instance of the fast paths,
         // with record kind, format and stride known at compile time
         // (also the compact local form and generated ops: the other batch shapes)
-        u32 fast = kind == REC_RC ? fast_txn(pos, REC_RC, 0u, h, gop)
+        u32 fast = tried ? 0u
                  : kind == REC_LC ? fast_txn(pos, REC_LC, 0u, h, gop)
                  : gen ? fast_txn(pos, REC_LTXN, 1u, h, gop) : fast_txn(pos, kind, 0u, h, gop);
 #ifdef CRDT_PROF
