@@ -95,7 +95,9 @@ CRDT_HD bool can_append(const Span& a, const Span& b) {  // span.rs:47-53
 // The same test as early exits, for wave-uniform operands (the replay's scalar code): a branch per
 // condition instead of lane-mask booleans.  (can_append stays branch-free for lane-parallel use.)
 CRDT_HD bool can_append_u(const Span& a, const Span& b) {
-  if ((a.len > 0) != (b.len > 0)) return false;
+  // (a.len > 0) == (b.len > 0) as integer sign bits ((u32)-len >> 31 = len > 0 for |len| < 2^31):
+  // one compare and branch instead of two booleans combined as lane masks
+  if (((u32)(-a.len) >> 31) != ((u32)(-b.len) >> 31)) return false;
   if (b.order != a.order + slen(a)) return false;
   if (b.ol != b.order - 1) return false;
   return b.orr == a.orr;

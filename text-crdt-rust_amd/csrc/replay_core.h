@@ -338,7 +338,8 @@ struct Replayer {
   // ------------------------------------------------------------------ leaf cache
   CRDT_HD void commit() {
     u32 lf = g(C_LEAF);
-    if (lf == INVALID || !g(C_DIRTY)) return;
+    if (lf == INVALID) return;
+    if (!g(C_DIRTY)) return;
     w.cache_store(leafp(lf));
     dir_set_cached_vis(g(C_NOW));
     p(C_DIRTY, 0);
@@ -490,7 +491,8 @@ struct Replayer {
     u32 lf = w.ld(w.at(lof(), order));
     // (the fast paths leave the entries of delete orders unwritten: any value may be read there,
     // so a leaf id is trusted only if it exists, and then only if the order is found in it)
-    if (lf >= g(S_N_LEAVES) || lf == cl) return false;
+    if (lf >= g(S_N_LEAVES)) return false;
+    if (lf == cl) return false;
     if (load) {
       ensure(lf);
       idx = w.cfind_order(g(C_N), order);
@@ -1270,7 +1272,9 @@ struct Replayer {
     u32 per = per_txn(remote), rn = rec_n();
     u32 pos0 = g(T_RB_BASE) + b0;
     u32 end = g(T_RB_BASE) + nv;  // records scanned so far: [pos0, end)
-    while ((pos0 + (nt + 1u) * per > end) & (end < rn)) {  // the run reaches the end: scan on
+    while (true) {  // the run reaches the end: scan on
+      if (pos0 + (nt + 1u) * per <= end) break;
+      if (end >= rn) break;
       u32 last = pos0 + (nt - 1u) * per;
       u32 n = rn - last < 64u ? rn - last : 64u;
       u32 t2, l0;
@@ -1284,13 +1288,17 @@ struct Replayer {
   }
   CRDT_HD u32 fast_typing(u32 b0, u32 nv, u32 remote, u32 idx, u32 orr, u32 agent, const Rec& o, u32 first) {
     Span e = w.cget(idx);
-    if (!((e.len > 0) & (e.order + (u32)e.len == first) & (e.orr == orr))) return 0;
+    if (e.len <= 0) return 0;
+    if (e.order + (u32)e.len != first) return 0;
+    if (e.orr != orr) return 0;
     u32 total;
     u32 nt = typing_run(b0, nv, remote, agent, o.w1, o, total);
     if (g(K_MAP) - first < total) return 0;     // capacity: the general path stops exactly
     map_fill(first, total, g(C_LEAF));   // notify (doc.rs:143-153)
     e.len += (i32)total;
-    set(idx, e);
+    w.cset(idx, e);  // (e is visible: the count grows by total)
+    p(C_NOW, g(C_NOW) + total);
+    p(C_DIRTY, 1u);
     inc(S_N_ITEMS, total);
     fast_txn_commit(first, total);
     return nt * per_txn(remote);
@@ -1310,26 +1318,31 @@ struct Replayer {
     u32 m = ha + hc;
     u32 pre = 0;
     Span nx{0, 0, 0, 0};
-    if (m != 0u && idx + 1u < n) {
-      nx = w.cget(idx + 1u);
-      Span last = m == 2u ? pc : x0;
-      if (can_append_u(last, nx)) {
-        nx.order = last.order;  // YjsSpan::prepend keeps origin_left (span.rs:61-64)
-        nx.len += last.len;
-        pre = 1;
-        m -= 1u;
+    if (m != 0u) {
+      if (idx + 1u < n) {
+        nx = w.cget(idx + 1u);
+        Span last = m == 2u ? pc : x0;
+        if (can_append_u(last, nx)) {
+          nx.order = last.order;  // YjsSpan::prepend keeps origin_left (span.rs:61-64)
+          nx.len += last.len;
+          pre = 1;
+          m -= 1u;
+        }
       }
     }
     if (n + m > (u32)L) return 0;
-    set(idx, ha ? pa : dd);
-    if (pre) set(idx + 1u, nx);
+    // entry writes straight to the cache; the visible count drops by exactly the l deleted items
+    w.cset(idx, ha ? pa : dd);
+    if (pre) w.cset(idx + 1u, nx);
     if (m) {
       w.cache_shift_right(idx + 1u, n, m);
       p(C_N, n + m);
-      set(idx + 1u, x0);
-      if (m == 2u) set(idx + 2u, pc);
+      w.cset(idx + 1u, x0);
+      if (m == 2u) w.cset(idx + 2u, pc);
       inc(S_N_ENTRIES, m);
     }
+    p(C_NOW, g(C_NOW) - l);
+    p(C_DIRTY, 1u);
     return 1;
   }
   // A run of k >= 2 one-item deletes in closed form (the per-op rules of leaf_delete, solved once):
@@ -1438,7 +1451,10 @@ struct Replayer {
         u32 rn = rec_n();
         u32 pos0 = g(T_RB_BASE) + b0;
         u32 end = g(T_RB_BASE) + nv;
-        while ((k < room) & (pos0 + (k + 1u) * per > end) & (end < rn)) {
+        while (true) {
+          if (k >= room) break;
+          if (pos0 + (k + 1u) * per <= end) break;
+          if (end >= rn) break;
           u32 last = pos0 + (k - 1u) * per;
           u32 n = rn - last < 64u ? rn - last : 64u;
           u32 n2 = w.delete_scan_at(w.at(recs(), last), n, remote, cpt, agent, delta);
@@ -1547,19 +1563,24 @@ struct Replayer {
     u32 len = (u32)item.len;
     u32 has_rem = off < slen(e);
     u32 space = 1u + has_rem;
-    if ((n + space > (u32)L) | (g(K_MAP) - item.order < len)) return 0;
+    if (n + space > (u32)L) return 0;
+    if (g(K_MAP) - item.order < len) return 0;
+    // entry writes straight to the cache (truncating e keeps its visible items in e + rem); the
+    // visible count grows by exactly the item's len
     if (has_rem) {
       Span rem = truncate(e, off);
-      set(idx, e);
+      w.cset(idx, e);
       w.cache_shift_right(idx + 1u, n, 2u);
-      set(idx + 2u, rem);
+      w.cset(idx + 2u, rem);
     } else {
       w.cache_shift_right(idx + 1u, n, 1u);
     }
     p(C_N, n + space);
     inc(S_N_ENTRIES, space);
     map_fill(item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
-    set(idx + 1u, item);
+    w.cset(idx + 1u, item);
+    p(C_NOW, g(C_NOW) + len);
+    p(C_DIRTY, 1u);
     inc(S_N_ITEMS, len);
     return 1;
   }
@@ -1660,7 +1681,7 @@ struct Replayer {
       if (g(C_N) + 1u + (c.off < el) > (u32)L) {
         // integrate stops at once here (checked above), so apply_txn would only insert_internal
         // the item, splitting the leaf (mutations.rs:17-179): do that here when a leaf is free
-        if ((g(K_LEAF) - g(S_N_LEAVES) >= 2u) & (g(K_MAP) - first >= l)) {
+        if ((g(K_LEAF) - g(S_N_LEAVES) >= 2u) && (g(K_MAP) - first >= l)) {
           insert_items(item, Span{0, 0, 0, 0}, Span{0, 0, 0, 0}, 1u, c, INVALID);
           inc(S_N_ITEMS, l);
           fast_txn_commit(first, l);
