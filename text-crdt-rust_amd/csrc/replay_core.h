@@ -1363,12 +1363,29 @@ struct Replayer {
     u32 room = (u32)L - n;  // new entries the leaf can take
     u32 delta;
     if (back) {
-      if (off + 1u != (u32)E.len) return 0;  // not from the entry's last item
-      u32 p0 = has_nx && can_append_u(Span{t1, t1 - 1u, orr, -1}, N0);
+      // Backspacing from inside E (not its last item): the run's first delete splits E after its
+      // target, so E[off+1..] becomes the entry after E; it is visible and the deleted items are
+      // not, so nothing prepends onto it (p0 = 0) and the run is the end-of-entry case on
+      // E[..off+1] with one entry more (mutate_entry, mutations.rs:227-277, gives the same leaf).
+      u32 mid = off + 1u != (u32)E.len ? 1u : 0u;
+      u32 p0 = 0u;
+      if (mid) {
+        if (room == 0u) return 0;
+        room -= 1u;
+      } else if (has_nx) {
+        p0 = can_append_u(Span{t1, t1 - 1u, orr, -1}, N0) ? 1u : 0u;
+      }
       u32 kmax = 2u * room + p0;
       k = k < off ? k : off;  // E keeps its first item (deleting it is a different shape)
       k = k < kmax ? k : kmax;
       if (k < 2u) return 0;
+      if (mid) {
+        Span pc = truncate(E, off + 1u);  // (E's visible items stay in E + pc)
+        w.cache_shift_right(idx + 1u, n, 1u);
+        w.cset(idx + 1u, pc);
+        n += 1u;
+        inc(S_N_ENTRIES, 1u);
+      }
       delta = p0 ? k / 2u : (k + 1u) / 2u;  // new entries F_1..F_delta, newest first after E
       w.cache_shift_right(idx + 1u, n, delta);
       w.cset_lanes(idx + 1u, idx + 1u + delta, [&](u32 lane) {
