@@ -19,6 +19,7 @@ import sys
 
 SYM = "_ZN4crdt8k_replayILi32EEEvNS_5PoolsEjjjPKj"
 FILTER = int(os.environ.get("FILTER_CALL_LINE", "0"))
+FN = os.environ.get("FILTER_FN", "")  # print this function's instructions (address, count/op)
 MNS = tuple(x for x in os.environ.get("FILTER_MN", "").split(",") if x)  # only these mnemonic prefixes  # only code inlined from a call at this line
 
 
@@ -267,6 +268,8 @@ def main():
                     else "lane" if mn.startswith(("v_readlane", "v_writelane", "v_readfirstlane"))
                     else "valu" if mn.startswith("v_") else "mem")
             fn = ch[-1].name if ch else SYM
+            if FN and FN in fn:
+                print(f"  {a:#x} {cnt / float(sys.argv[6]):6.3f} {mn:24s} {fl}:{ln}")
             kinds[kind] += cnt
             by_mn[mn] += cnt
             by_line[(fl, ln)][kind] += cnt

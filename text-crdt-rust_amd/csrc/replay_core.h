@@ -1773,7 +1773,20 @@ struct Replayer {
         // the remote-batch hot loop: compact remote txns through one fast-path instance, in a loop
         // of their own (its registers do not meet the other record kinds' paths at every txn)
         u32 fast;
-        while ((fast = fast_txn(pos, REC_RC, 0u, h, Rec{0, 0, 0, 0})) != 0u) {
+        while (true) {
+#ifdef CRDT_PROF
+          u64 t0 = w.clock();
+          fast = fast_txn(pos, REC_RC, 0u, h, Rec{0, 0, 0, 0});
+          u32 dt = prof_mode == 0u ? (u32)(w.clock() - t0) : prof_mode == 1u ? 1u : fast;
+          if (prof_mode != 3u && fast) {
+            if (prof_cat == 0u) inc(S_PROF0, dt);
+            else if (prof_cat == 2u) inc(S_PROF2, dt);
+            else inc(S_PROF3, dt);
+          }
+#else
+          fast = fast_txn(pos, REC_RC, 0u, h, Rec{0, 0, 0, 0});
+#endif
+          if (!fast) break;
           pos += fast;
           if (pos >= rn) break;
           h = rec(pos);

@@ -71,8 +71,8 @@ struct WaveGPU {
   __device__ __forceinline__ u32 xg(u32 f) const { return f < 64 ? rdlane(x0, f) : rdlane(x1, f - 64); }
   __device__ __forceinline__ void xs(u32 f, u32 v) {  // v_writelane (no lane mask to keep live)
     u32 sv = uni(v);  // folds away for values the compiler already knows are uniform
-    if (f < 64) asm("v_writelane_b32 %0, %1, %2" : "+v"(x0) : "s"(sv), "n"(f));
-    else asm("v_writelane_b32 %0, %1, %2" : "+v"(x1) : "s"(sv), "n"(f - 64));
+    if (f < 64) x0 = wrlane(x0, sv, f);
+    else x1 = wrlane(x1, sv, f - 64);
   }
   // Element idx (x M) of a table, the byte offset computed in a VGPR: the compiler then addresses
   // it as table base (SGPR pair) + 32-bit VGPR offset -- one or two VALU ops -- instead of the
