@@ -1451,8 +1451,14 @@ struct Replayer {
         if ((o.w1 & 0xFFFFu) != agent) break;
         if (o.w2 - key >= g(T_AGL_LEN)) break;
       }
-      Rec o2 = op_at(b0 + per, remote);
-      u32 delta = remote ? o2.w2 - o.w2 : o2.w1 - o.w1;
+      u32 delta;
+      if (cpt) {  // compact records: the next txn's target seq (RC w2) / pos (LC w1) read directly
+        Rec r2 = w.rec_get(b0 + per);
+        delta = remote ? r2.w2 - o.w2 : r2.w1 - o.w1;
+      } else {
+        Rec o2 = op_at(b0 + per, remote);
+        delta = remote ? o2.w2 - o.w2 : o2.w1 - o.w1;
+      }
       back = opq(delta == 0xFFFFFFFFu ? 1u : 0u);
       if (!back) {
         if (delta != (remote ? 1u : 0u)) break;
@@ -1617,8 +1623,7 @@ struct Replayer {
       // run() read the record at pos through the window (gh): a compact txn is that one record
       b0 = pos - g(T_RB_BASE);
       if (cpt) {
-        if (remote) expand_rc(h, h, o, pr);
-        else expand_lc(h, h, o);
+        if (!remote) expand_lc(h, h, o);  // (RC is decoded directly below)
       } else {
         if (rn - pos < per) return 0;  // (rec() left the whole txn inside the window: b0 <= 61)
         h = w.rec_get(b0);
@@ -1634,7 +1639,31 @@ struct Replayer {
     u32 first = g(S_NEXT_ORDER);
     u32 agent, l, ins, ol = 0, orr = ROOT_ORDER;
     Cursor c;
-    if (remote) {
+    if (remote && cpt) {
+      // RC: the compact record's fields directly (expand_rc's header, op and parent, without its
+      // origin-agent selects): author, seq, len, del; origins / target are the author's own items
+      // (a seq of 0xFFFFFFFF names ROOT) and the one parent is (author, seq - 1), so once
+      // fast_txn_ok has matched the author with the cached agent, every lookup is a tail check
+      Rec r = gh;
+      agent = r.w0 & 0xFFFFu;
+      u32 seq = r.w1;
+      l = rc_len(r);
+      u32 del = (r.w0 >> 27) & 1u;
+      ins = del ^ 1u;
+      u32 ra = r.w3 == 0xFFFFFFFFu ? ROOT_AGENT : agent;
+      o = del ? Rec{(REC_RDEL << 28) | l, agent, r.w2, 0u} : Rec{(REC_RINS << 28) | l, agent | (ra << 16), r.w2, r.w3};
+      if (l == 0u) return 0;
+      if (!fast_txn_ok(agent, seq, first)) return 0;
+      if (r.w2 == 0xFFFFFFFFu) return 0;                   // origin_left / target ROOT
+      if (!seq_to_order(agent, r.w2, ol)) return 0;        // (agent == T_AG_ID: a valid agent)
+      if (ins) {
+        if (r.w3 != 0xFFFFFFFFu) {
+          if (!seq_to_order(agent, r.w3, orr)) return 0;
+        }
+      }
+      if (!find_order(ol, true, c)) return 0;  // doc.rs:101-136 (loads the item's leaf)
+      c.off += ins;                             // get_cursor_after
+    } else if (remote) {
       agent = h.w1 & 0xFFFFu;
       u32 seq = h.w2;
       l = o.w0 & 0x0FFFFFFFu;
