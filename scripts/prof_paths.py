@@ -37,4 +37,4 @@ for i, k in enumerate(names):
     c, calls, tx = view["cycles"][i], view["calls"][i], view["txns"][i]
     print(f"  {k:8s} cycles {c:.4g} ({c / tot:.1%})  calls {calls:.0f}  txns {tx:.0f}  cycles/call {c / max(calls, 1):.0f}  cycles/txn {c / max(tx, 1):.0f}")
 s = np.array([e.debug_state(d) for d in range(3, n, 4 * max(1, n // 256))]).astype(np.float64)[:, P0:P0 + 4].mean(axis=0)
-print(f"  delete calls {s[3]:.0f}: cut by entry/room {s[0]:.0f}, cut by leaf {s[1]:.0f}, single-delete calls {s[2]:.0f}")
+print(f"  delete-call cycles by part: run detection {s[0]:.4g}, first segment {s[1]:.4g}, leaf-split loop {s[2]:.4g}, tail {s[3]:.4g}")

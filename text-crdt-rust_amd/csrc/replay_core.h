@@ -1429,6 +1429,9 @@ struct Replayer {
   // would (leaf_delete); the RLE tables, the order map and the txn log are updated once for the
   // run.  Returns records consumed (0: nothing applied).
   CRDT_HD u32 fast_deletes(u32 b0, u32 nv, u32 remote, u32 agent, u32 idx, u32 off, u32 l, u32 first, const Rec& o) {
+#ifdef CRDT_PROF
+    u64 pt0 = w.clock();  // detail (prof_mode 3): cycles of run detection / first segment / leaf-split loop / tail
+#endif
     u32 per = per_txn(remote);
     u32 t1 = w.cget_order(idx) + off;
     u32 split_first = 0;
@@ -1486,17 +1489,23 @@ struct Replayer {
           k += n2 - 1u;
         }
 #ifdef CRDT_PROF
-        if (prof_mode == 3u && k > room) inc(S_PROF0);  // detail: run cut by the entry / item_orders room
+
 #endif
         k = k < room ? k : room;
       }
     } while (0);
 #ifdef CRDT_PROF
-    if (prof_mode == 3u) { inc(S_PROF3); if (k == 1u) inc(S_PROF2); }  // detail: delete calls, single deletes
+
 #endif
     if (g(K_MAP) - first < k * l) return 0;
     if (g(K_DEL) - g(S_N_DEL) < k) return 0;
+#ifdef CRDT_PROF
+    u64 pt1 = w.clock();
+#endif
     u32 done = split_first ? 0u : delete_segment(idx, off, t1, k, back, l);
+#ifdef CRDT_PROF
+    u64 pt2 = w.clock();
+#endif
     // The leaf ran out of room (or the run reached a shape the segment does not take): the next
     // delete goes the general way -- mutate_entry + insert_internal, splitting the leaf -- and the
     // rest of the run continues from wherever its next target now lives.
@@ -1519,10 +1528,10 @@ struct Replayer {
       if (c.off + l > (u32)el) break;
       done += delete_segment(c.idx, c.off, t2, k - done, back, l);
     }
-    if (done == 0u) return 0;
 #ifdef CRDT_PROF
-    if (prof_mode == 3u && done < k) inc(S_PROF1);  // detail: run cut by the leaf (closed form / op by op)
+    u64 pt3 = w.clock();
 #endif
+    if (done == 0u) return 0;
     if (back) {  // doc.rs:305-308 / 420-423: backspaced targets never coalesce: one run each
       append_delete(first, t1, 1u);
       if (done > 1u) {
@@ -1538,6 +1547,12 @@ struct Replayer {
       append_delete(first, t1, done * l);  // forward deletes coalesce into one run (Rle::append)
     }
     fast_txn_commit(first, done * l);  // (delete orders name no item: no order -> leaf entries)
+#ifdef CRDT_PROF
+    if (prof_mode == 3u) {
+      inc(S_PROF0, (u32)(pt1 - pt0)); inc(S_PROF1, (u32)(pt2 - pt1));
+      inc(S_PROF2, (u32)(pt3 - pt2)); inc(S_PROF3, (u32)(w.clock() - pt3));
+    }
+#endif
     return done * per;
   }
   // Up to k one-item deletes of a run (the first at `off` of entry idx, target t), in closed form
@@ -1558,23 +1573,81 @@ struct Replayer {
     return done;
   }
   // One delete of l items at offset `off` of visible entry idx, exactly as apply_txn does it:
-  // mutate_entry (mutations.rs:227-277: the entry's first part stays, the deleted piece and the
-  // remainder are inserted after it) and insert_internal, splitting the leaf when it is full
-  // (mutations.rs:17-179, split_at :623-669).  The caller checked that a leaf is free.
+  // mutate_entry (mutations.rs:227-277: the entry's first part stays at idx, the deleted piece and
+  // the visible remainder go after it) and insert_internal (mutations.rs:17-179), splitting the
+  // leaf when the pieces do not fit (split_at, :623-669).  insert_internal's steps specialised to
+  // these pieces: the first part never absorbs the next piece (one is visible, the other deleted),
+  // at most the last piece prepends onto the entry after idx (YjsSpan::prepend keeps origin_left),
+  // and the rest (m <= 2 entries) is inserted at idx + 1.  The caller checked that a leaf is free.
   CRDT_HD void delete_general(u32 idx, u32 off, u32 l) {
     Span e = w.cget(idx);
-    u32 elen = slen(e);
-    u32 ha = off > 0u, hc = 0u;
-    Span pa{0, 0, 0, 0}, pc{0, 0, 0, 0};
-    if (ha) { elen -= off; pa = truncate_keeping_right(e, off); }
-    if (l < elen) { pc = truncate(e, l); hc = 1u; }
-    e.len = -e.len;
-    Span first_part = ha ? pa : e;
-    set(idx, first_part);
-    Cursor c{g(C_LEAF), idx, slen(first_part)};
-    Span a0 = ha ? e : pc;
-    u32 n = ha ? 1u + hc : hc;
-    insert_items(a0, pc, Span{0, 0, 0, 0}, n, c, g(C_LEAF));  // (n <= 2: cannot fail)
+    u32 n = g(C_N);
+    u32 t = e.order + off;
+    u32 ha = off > 0u ? 1u : 0u, hc = off + l < (u32)e.len ? 1u : 0u;
+    Span pa{e.order, e.ol, e.orr, (i32)off};
+    Span dd{t, ha ? t - 1u : e.ol, e.orr, -(i32)l};
+    Span pc{t + l, t + l - 1u, e.orr, e.len - (i32)(off + l)};
+    Span x0 = ha ? dd : pc;  // pieces after the first part: [x0, pc][:m]
+    u32 m = ha + hc;
+    u32 pre = 0, pre_vis = 0;
+    Span nx{0, 0, 0, 0};
+    if (m != 0u) {
+      if (idx + 1u < n) {
+        nx = w.cget(idx + 1u);
+        Span last = m == 2u ? pc : x0;
+        if (can_append_u(last, nx)) {
+          nx.order = last.order;
+          nx.len += last.len;
+          pre = 1;
+          pre_vis = last.len > 0 ? (u32)last.len : 0u;
+          m -= 1u;
+        }
+      }
+    }
+    w.cset(idx, ha ? pa : dd);
+    if (pre) w.cset(idx + 1u, nx);
+    // the cache now holds everything but the m unplaced pieces: e's l deleted items and the
+    // visible pieces still to place are off its count
+    u32 unplaced_vis = (hc && !pre) ? (u32)pc.len : 0u;
+    p(C_NOW, g(C_NOW) - l - unplaced_vis);
+    p(C_DIRTY, 1u);
+    (void)pre_vis;
+    if (m == 0u) return;
+    inc(S_N_ENTRIES, m);
+    u32 ci = idx + 1u;
+    u32 home = g(C_LEAF);
+    u32 leaf = home;
+    u32 at = ci;
+    if (n + m > (u32)L) {
+      u32 follow = ci >= (u32)L / 2u ? 1u : 0u;
+      u32 moved = n - ci;
+      u32 succ = g(C_SUCC), succ_ord = g(C_SUCC_ORD);  // the old leaf's successor follows nl
+      u32 nl = split_at(ci, follow ? m : 0u);
+      if (follow) {  // the pieces lead the new leaf, which becomes the cached one (insert_items)
+        u32 nblk = g(C_BLK), ni = g(C_I) + 1u;
+        commit();
+        w.cache_from_moved();
+        u32 v = w.cache_vis_from(0u);
+        p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 1u); p(C_VS_OK, 0);
+        p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
+        p(C_N, m + moved);
+        leaf = nl;
+        at = 0u;
+      } else {
+        p(C_N, ci + m);
+      }
+    } else {
+      w.cache_shift_right(ci, n, m);
+      p(C_N, n + m);
+    }
+    notify(x0, leaf, home);
+    w.cset(at, x0);
+    if (m == 2u) {
+      notify(pc, leaf, home);
+      w.cset(at + 1u, pc);
+    }
+    p(C_NOW, g(C_NOW) + unplaced_vis);
   }
   // Insert one item run right after the cursor (idx, off), 0 < off <= |entry|, when integrate
   // stops at once and the run cannot be appended: insert_internal (mutations.rs:17-179) splits
