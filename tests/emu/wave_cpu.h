@@ -286,6 +286,7 @@ struct WaveCPU {
     len_idx = p[idx].len;
     return t;
   }
+  void st_span(Span* p, const Span& s) const { *p = s; }
   void st_probe(uint4* p, u32 a, u32 s, u32 ps, u32 dl) const { *p = make_uint4(a, s, ps, dl); }
   bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
     u32 acc = 0;

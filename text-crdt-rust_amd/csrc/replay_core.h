@@ -521,7 +521,9 @@ struct Replayer {
   // ------------------------------------------------------------------ leaf mutation
   // mutations.rs:623-669 split_at: [idx, n) of the cached leaf moves to a new leaf (after
   // `padding` empty slots), which is linked right after the cached leaf.  Returns its id.
-  CRDT_HD u32 split_at(u32 idx, u32 padding) {
+  // extra_vis: visible items the caller puts into the new leaf's padding slots in HBM itself
+  // (counted in its directory slot, its group and the document length here)
+  CRDT_HD u32 split_at(u32 idx, u32 padding, u32 extra_vis = 0u) {
     u32 nl = g(S_N_LEAVES);
     p(S_N_LEAVES, nl + 1);
     u32 n = g(C_N);
@@ -548,9 +550,10 @@ struct Replayer {
       if (i >= 32) { blk = nb; i -= 32; gg = gg + 1; p(C_BLK, nb); p(C_I, i); }
       cnt = 32;
     }
-    w.blk_insert(dleaf(blk), dvis(blk), cnt, i + 1, nl, stolen, sol(), blk);
+    w.blk_insert(dleaf(blk), dvis(blk), cnt, i + 1, nl, stolen + extra_vis, sol(), blk);
     // the cached leaf's directory count loses `stolen` (moved to nl); group total unchanged
-    w.root_set(gg, blk, cnt + 1, w.root_vis(gg));
+    w.root_set(gg, blk, cnt + 1, w.root_vis(gg) + extra_vis);
+    if (extra_vis) inc(S_LEN, extra_vis);
     u32 cv = g(C_VIS) - stolen;
     w.st(dvis(blk) + i, cv);
     p(C_VIS, cv);
@@ -1518,7 +1521,7 @@ struct Replayer {
       i32 el = w.cget_len(c.idx);
       if (el <= 0) break;
       if (c.off + l > (u32)el) break;
-      delete_general(c.idx, c.off, l);
+      delete_general(c.idx, c.off, l, back);
       done++;
       if (done == k) break;
       u32 t2 = back ? t1 - done : t1 + done;
@@ -1579,7 +1582,9 @@ struct Replayer {
   // these pieces: the first part never absorbs the next piece (one is visible, the other deleted),
   // at most the last piece prepends onto the entry after idx (YjsSpan::prepend keeps origin_left),
   // and the rest (m <= 2 entries) is inserted at idx + 1.  The caller checked that a leaf is free.
-  CRDT_HD void delete_general(u32 idx, u32 off, u32 l) {
+  // back: a backspace run goes on at the item before t, in the first part at idx: a split that
+  // would move the cache to the new leaf writes the pieces there in HBM and keeps the old leaf.
+  CRDT_HD void delete_general(u32 idx, u32 off, u32 l, u32 back) {
     Span e = w.cget(idx);
     u32 n = g(C_N);
     u32 t = e.order + off;
@@ -1622,6 +1627,17 @@ struct Replayer {
       u32 follow = ci >= (u32)L / 2u ? 1u : 0u;
       u32 moved = n - ci;
       u32 succ = g(C_SUCC), succ_ord = g(C_SUCC_ORD);  // the old leaf's successor follows nl
+      if (follow & back) {  // the pieces lead the new leaf in HBM; the old leaf stays cached
+        u32 nl = split_at(ci, m, unplaced_vis);
+        Span* q = leafp(nl);
+        w.st_span(q, x0);
+        notify(x0, nl, home);
+        if (m == 2u) {
+          w.st_span(q + 1, pc);
+          notify(pc, nl, home);
+        }
+        return;
+      }
       u32 nl = split_at(ci, follow ? m : 0u);
       if (follow) {  // the pieces lead the new leaf, which becomes the cached one (insert_items)
         u32 nblk = g(C_BLK), ni = g(C_I) + 1u;

@@ -686,6 +686,9 @@ struct WaveGPU {
     len_idx = (i32)rdlane((u32)n, idx);
     return wave_sum(l < idx && l < (u32)L && n > 0 ? (u32)n : 0u);
   }
+  __device__ __forceinline__ void st_span(Span* p, const Span& s) const {  // every lane stores the same entry
+    *(uint4*)p = make_uint4(s.order, s.ol, s.orr, (u32)s.len);
+  }
   __device__ __forceinline__ void st_probe(uint4* p, u32 a, u32 s, u32 ps, u32 dl) const {
     *p = make_uint4(a, s, ps, dl);  // every lane stores the same values
   }
