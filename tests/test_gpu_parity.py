@@ -356,3 +356,35 @@ def test_long_document_publish_chains():
             assert int(e.digests()[i]) == o.digest()
             check_queries_sampled(e, i, o, n=1 << 14)
         assert e.export(0)["canon"].shape[0] <= 2
+
+
+def test_pos_to_loc_chunks_staged_and_mixed():
+    """pos -> loc answers of the chunked kernel (k_pos_to_loc_blk: 4,096-query chunks; a chunk of one
+    document searches its visible prefix staged in LDS, any other chunk per thread in HBM) against
+    the oracle: uniform chunks, a chunk straddling two documents, interleaved documents and
+    out-of-range positions / documents in one batch."""
+    names = ["sveltecomponent", "rustcode", "automerge-paper"]
+    e = crdt_amd.Engine(len(names), 32)
+    orc = []
+    for d, name in enumerate(names):
+        t = load_trace(name)
+        a = e.agent_intern([d], ["jeremy"])
+        assert e.apply_trace([d], int(a[0]), t.counts, t.patches)[0] == 0
+        o = OracleDoc(32, 16)
+        o.apply_trace(o.agent("jeremy"), t.counts, t.patches)
+        orc.append(o)
+    rng = np.random.default_rng(11)
+    lens = [len(o) for o in orc]
+    # 2.5 uniform chunks of document 2, 1.5 of document 0 (a chunk straddles them), then mixed
+    d_u = np.concatenate([np.full(10240, 2), np.full(6144, 0)])
+    d_m = rng.integers(0, 4, 9000)  # document 3 does not exist
+    docs = np.concatenate([d_u, d_m]).astype(np.uint32)
+    pos = np.array([rng.integers(0, (lens[d] if d < 3 else 10) + 3) for d in docs], np.uint32)
+    ga, gs = e.pos_to_loc(docs, pos)
+    for d in range(4):
+        m = docs == d
+        if d == 3:
+            assert (ga[m] == 0xFFFF).all() and (gs[m] == 0xFFFFFFFF).all()
+            continue
+        oa, os_ = orc[d].pos_to_loc(pos[m])
+        assert np.array_equal(ga[m], oa) and np.array_equal(gs[m], os_), d

@@ -937,6 +937,8 @@ int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
   // the replay's LDS root may take a workgroup's whole 160 KiB (one wave per workgroup)
   (void)hipFuncSetAttribute((const void*)k_replay<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<32>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);
+  (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<4>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);
   (void)hipFuncSetAttribute((const void*)k_pub_index, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pubx_lds_bytes(PUBX_MAX_WORDS));
   for (auto& x : e->ev)
@@ -1310,9 +1312,17 @@ int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
     if (r) return r;
   }
   if (!n) return 0;
-  u32 blocks = (u32)std::min<u64>((n + 255) / 256, 8192);
-  if (e->L == 32) hipLaunchKernelGGL(k_pos_to_loc<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
-  else hipLaunchKernelGGL(k_pos_to_loc<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+  static const bool per_thread = getenv("CRDT_QUERY_PER_THREAD") != nullptr;  // (A/B of the two kernels)
+  if (per_thread) {
+    u32 blocks = (u32)std::min<u64>((n + 255) / 256, 8192);
+    if (e->L == 32) hipLaunchKernelGGL(k_pos_to_loc<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+    else hipLaunchKernelGGL(k_pos_to_loc<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+  } else {  // chunks of QBLK_Q queries; a one-document chunk searches its vpos staged in LDS
+    u64 blocks = (n + QBLK_Q - 1) / QBLK_Q;
+    if (blocks > 0x7FFFFFFFull) return CRDT_E_ARG;
+    if (e->L == 32) hipLaunchKernelGGL(k_pos_to_loc_blk<32>, dim3((u32)blocks), dim3(QBLK_T), QBLK_LDS, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+    else hipLaunchKernelGGL(k_pos_to_loc_blk<4>, dim3((u32)blocks), dim3(QBLK_T), QBLK_LDS, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }

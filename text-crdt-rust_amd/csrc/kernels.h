@@ -850,6 +850,146 @@ __global__ void k_pos_to_loc(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* d
   }
 }
 
+// pos -> loc for a query batch whose queries come in runs per document (the usual shape: a
+// document's cursors, or a batch sorted by document): block b answers queries
+// [b * QBLK_Q, (b + 1) * QBLK_Q).  When they all name one document whose visible prefix vpos fits
+// QBLK_MAX entries, the block stages vpos in LDS with coalesced loads (each entry read from HBM
+// once per block instead of ~log2(spans) dependent gathers per query) and every query's binary
+// search runs in LDS; any other chunk answers thread by thread from HBM, as k_pos_to_loc.
+#define QBLK_Q 4096u
+#define QBLK_T 1024u    // threads per block (16 waves: one block per CU holds the LDS)
+#define QBLK_MAX 36864u  // 144 KiB of LDS
+#define QBLK_CWO 512u    // client_with_order runs staged with it (8 KiB)
+#define QBLK_LDS (QBLK_MAX * 4u + QBLK_CWO * 16u)
+template <int L>
+__global__ __launch_bounds__(QBLK_T) void k_pos_to_loc_blk(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* doc, const u32* pos,
+                                                        u16* agent, u32* seq) {
+  extern __shared__ u32 s_vp[];
+  __shared__ u32 s_mixed;
+  const u32 t = threadIdx.x;
+  const u64 q0 = (u64)blockIdx.x * QBLK_Q;
+  const u64 q1 = q0 + QBLK_Q < nq ? q0 + QBLK_Q : nq;
+  const u32 d0 = doc[q0];
+  if (t == 0) s_mixed = 0;
+  __syncthreads();
+  u32 mixed = 0;
+#pragma unroll
+  for (u32 j = 0; j < QBLK_Q / QBLK_T; j++) {  // (unrolled: the loads are in flight together)
+    u64 q = q0 + (u64)j * QBLK_T + t;
+    mixed |= (q < q1 && doc[q] != d0) ? 1u : 0u;
+  }
+  if (mixed) s_mixed = 1;  // (any writer stores the same value)
+  __syncthreads();
+  bool staged = false;
+  u32 cn = 0, dlen = 0, ncwo = 0;
+  DocSeg seg{};
+  if (!s_mixed && d0 < n_docs) {
+    i32 stt = P.st[d0].status;
+    cn = O.canon_n[d0];
+    if ((stt == ST_OK || stt == ST_NEED_CAPACITY) && cn <= QBLK_MAX) {
+      seg = P.seg[d0];
+      dlen = O.len[d0];
+      ncwo = P.st[d0].n_cwo;
+      const u32* vp = O.vpos + seg.canon_base;
+      for (u32 i0 = 0; i0 < cn; i0 += QBLK_T * 16u) {  // 16 loads per thread in flight per step
+        u32 v[16];
+#pragma unroll
+        for (u32 u = 0; u < 16u; u++) {
+          u32 i = i0 + u * QBLK_T + t;
+          v[u] = i < cn ? vp[i] : 0u;
+        }
+#pragma unroll
+        for (u32 u = 0; u < 16u; u++) {
+          u32 i = i0 + u * QBLK_T + t;
+          if (i < cn) s_vp[i] = v[u];
+        }
+      }
+      staged = true;
+    }
+  }
+  __syncthreads();
+  if (!staged) {  // mixed chunk, long document or a failed one: per-thread search in HBM
+    for (u64 q = q0 + t; q < q1; q += QBLK_T) {
+      u32 d = doc[q], p = pos[q];
+      u16 a = 0xFFFF;
+      u32 sq = INVALID;
+      if (d < n_docs) {
+        i32 stt = P.st[d].status;
+        if ((stt == ST_OK || stt == ST_NEED_CAPACITY) && p < O.len[d]) {
+          DocSeg sg = P.seg[d];
+          const u32* vp = O.vpos + sg.canon_base;
+          u32 lo = 0, hi = O.canon_n[d];
+          while (lo < hi) {
+            u32 mid = (lo + hi) >> 1;
+            if (vp[mid] <= p) lo = mid + 1; else hi = mid;
+          }
+          u32 k = lo - 1;
+          u32 order = O.canon[sg.canon_base + k].order + (p - vp[k]);
+          const CwoRun* cw = P.cwo + sg.cwo_base;
+          i32 r = find_run(cw, P.st[d].n_cwo, order);
+          if (r >= 0) { a = (u16)cw[r].agent; sq = cw[r].seq + (order - cw[r].key); }
+        }
+      }
+      agent[q] = a;
+      seq[q] = sq;
+    }
+    return;
+  }
+  // 16 queries per thread in three sweeps, so that each sweep's independent loads are in flight
+  // together: binary searches in LDS, then the spans' first orders (corder, 4 B per span), then
+  // client_with_order runs (staged in LDS too when the table is short)
+  const u32* co = O.corder + seg.canon_base;
+  const CwoRun* cw = P.cwo + seg.cwo_base;
+  CwoRun* s_cw = (CwoRun*)(s_vp + QBLK_MAX);
+  const bool cw_lds = ncwo <= QBLK_CWO;
+  if (cw_lds) {
+    for (u32 i = t; i < ncwo; i += QBLK_T) s_cw[i] = cw[i];
+  }
+  __syncthreads();
+  constexpr u32 QPT = QBLK_Q / QBLK_T;
+  u32 kk[QPT], pp[QPT];
+#pragma unroll
+  for (u32 j = 0; j < QPT; j++) {
+    u64 q = q0 + (u64)j * QBLK_T + t;
+    pp[j] = q < q1 ? pos[q] : INVALID;
+    kk[j] = 0u;
+  }
+  // the 16 searches in lockstep (the halving sequence depends only on cn), so each step's 16 LDS
+  // reads are in flight together: kk = the last span whose vpos <= p
+  for (u32 n = cn; n > 1u;) {
+    u32 half = n >> 1;
+#pragma unroll
+    for (u32 j = 0; j < QPT; j++) kk[j] = s_vp[kk[j] + half] <= pp[j] ? kk[j] + half : kk[j];
+    n -= half;
+  }
+#pragma unroll
+  for (u32 j = 0; j < QPT; j++) {
+    u32 p = pp[j];
+    if (p < dlen) pp[j] = p - s_vp[kk[j]];  // (vpos[0] = 0 <= p: kk is a span)
+    else kk[j] = INVALID;
+  }
+#pragma unroll
+  for (u32 j = 0; j < QPT; j++) pp[j] = kk[j] != INVALID ? co[kk[j]] + pp[j] : INVALID;  // orders
+#pragma unroll
+  for (u32 j = 0; j < QPT; j++) {
+    u64 q = q0 + (u64)j * QBLK_T + t;
+    if (q >= q1) break;
+    u16 a = 0xFFFF;
+    u32 sq = INVALID;
+    if (kk[j] != INVALID) {
+      u32 order = pp[j];
+      i32 r = cw_lds ? find_run(s_cw, ncwo, order) : find_run(cw, ncwo, order);
+      if (r >= 0) {
+        CwoRun c = cw_lds ? s_cw[r] : cw[r];
+        a = (u16)c.agent;
+        sq = c.seq + (order - c.key);
+      }
+    }
+    agent[q] = a;
+    seq[q] = sq;
+  }
+}
+
 template <int L>
 __global__ void k_loc_to_pos(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* doc, const u16* agent, const u32* seq, u32* pos, u8* deleted) {
   for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (u64)gridDim.x * blockDim.x) {
