@@ -388,3 +388,16 @@ def test_pos_to_loc_chunks_staged_and_mixed():
             continue
         oa, os_ = orc[d].pos_to_loc(pos[m])
         assert np.array_equal(ga[m], oa) and np.array_equal(gs[m], os_), d
+    # loc -> pos through the same chunking (k_loc_to_pos_blk): staged and mixed chunks, unknown
+    # agents / seqs / documents
+    ag = rng.integers(0, 3, docs.shape[0]).astype(np.uint16)  # agent 0 is the only real one
+    sq = np.array([rng.integers(0, (orc[d].sizes()["next_order"] if d < 3 else 10) + 3) for d in docs], np.uint32)
+    gp, gd = e.loc_to_pos(docs, ag, sq)
+    for d in range(4):
+        m = docs == d
+        if d == 3:
+            assert (gd[m] == 2).all()
+            continue
+        op, od = orc[d].loc_to_pos(ag[m], sq[m])
+        assert np.array_equal(gd[m], od), d
+        assert np.array_equal(gp[m][od != 2], op[od != 2]), d

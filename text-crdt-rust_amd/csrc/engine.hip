@@ -939,6 +939,8 @@ int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
   (void)hipFuncSetAttribute((const void*)k_replay<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<32>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);
   (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<4>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);
+  (void)hipFuncSetAttribute((const void*)k_loc_to_pos_blk<32>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_W * 8u);
+  (void)hipFuncSetAttribute((const void*)k_loc_to_pos_blk<4>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_W * 8u);
   (void)hipFuncSetAttribute((const void*)k_pub_index, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)pubx_lds_bytes(PUBX_MAX_WORDS));
   for (auto& x : e->ev)
@@ -1335,8 +1337,16 @@ int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
   }
   if (!n) return 0;
   u32 blocks = (u32)std::min<u64>((n + 255) / 256, 8192);
-  if (e->L == 32) hipLaunchKernelGGL(k_loc_to_pos<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
-  else hipLaunchKernelGGL(k_loc_to_pos<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
+  static const bool per_thread = getenv("CRDT_QUERY_PER_THREAD") != nullptr;  // (A/B of the two kernels)
+  if (per_thread) {
+    if (e->L == 32) hipLaunchKernelGGL(k_loc_to_pos<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
+    else hipLaunchKernelGGL(k_loc_to_pos<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
+  } else {  // chunks of QBLK_Q queries; a one-document chunk ranks orders in its LDS-staged bitmap
+    u64 nb = (n + QBLK_Q - 1) / QBLK_Q;
+    if (nb > 0x7FFFFFFFull) return CRDT_E_ARG;
+    if (e->L == 32) hipLaunchKernelGGL(k_loc_to_pos_blk<32>, dim3((u32)nb), dim3(QBLK_T), QBLK_W * 8u, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
+    else hipLaunchKernelGGL(k_loc_to_pos_blk<4>, dim3((u32)nb), dim3(QBLK_T), QBLK_W * 8u, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }

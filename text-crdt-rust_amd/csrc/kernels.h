@@ -990,6 +990,124 @@ __global__ __launch_bounds__(QBLK_T) void k_pos_to_loc_blk(Pools P, PubOut O, u3
   }
 }
 
+// loc -> pos in the same 4,096-query chunks: a one-document chunk stages the used words of its
+// span-start bitmap and their prefix counts in LDS (coalesced), so order -> span rank is two LDS
+// reads; the agent's item_orders run, the rank -> span entry and the span itself are gathered in
+// sweeps with every thread's queries in flight together.  Other chunks: as k_loc_to_pos.
+#define QBLK_W 16384u  // bitmap words staged (+ as many prefix words: 128 KiB)
+template <int L>
+__global__ __launch_bounds__(QBLK_T) void k_loc_to_pos_blk(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* doc, const u16* agent,
+                                                         const u32* seq, u32* pos, u8* deleted) {
+  extern __shared__ u32 s_bw[];  // [0, used) bitmap words, [QBLK_W, QBLK_W + used) prefixes
+  __shared__ u32 s_mixed;
+  const u32 t = threadIdx.x;
+  const u64 q0 = (u64)blockIdx.x * QBLK_Q;
+  const u64 q1 = q0 + QBLK_Q < nq ? q0 + QBLK_Q : nq;
+  const u32 d0 = doc[q0];
+  if (t == 0) s_mixed = 0;
+  __syncthreads();
+  u32 mixed = 0;
+#pragma unroll
+  for (u32 j = 0; j < QBLK_Q / QBLK_T; j++) {
+    u64 q = q0 + (u64)j * QBLK_T + t;
+    mixed |= (q < q1 && doc[q] != d0) ? 1u : 0u;
+  }
+  if (mixed) s_mixed = 1;
+  __syncthreads();
+  bool staged = false;
+  DocState st{};
+  DocSeg seg{};
+  u32 used = 0, cn = 0;
+  if (!s_mixed && d0 < n_docs) {
+    st = P.st[d0];
+    used = st.next_order / 32u + 1u;
+    if ((st.status == ST_OK || st.status == ST_NEED_CAPACITY) && used <= QBLK_W) {
+      seg = P.seg[d0];
+      cn = O.canon_n[d0];
+      u32 nw = pub_words(seg.ord_cap);
+      const u32* bits = O.pub + seg.pub_base;
+      for (u32 i = t; i < used; i += QBLK_T) {
+        u32 b = i < nw ? bits[i] : 0u, c = i < nw ? bits[nw + i] : 0u;
+        s_bw[i] = b;
+        s_bw[QBLK_W + i] = c;
+      }
+      staged = true;
+    }
+  }
+  __syncthreads();
+  if (!staged) {
+    for (u64 q = q0 + t; q < q1; q += QBLK_T) {
+      u32 d = doc[q];
+      u32 ps = INVALID;
+      u8 dl = 2;
+      if (d < n_docs) {
+        DocState s = P.st[d];
+        if ((s.status == ST_OK || s.status == ST_NEED_CAPACITY) && agent[q] < s.n_agents) {
+          DocSeg sg = P.seg[d];
+          AgentRec A = P.agents[sg.agent_base + agent[q]];
+          const ARun* ar = P.arun + sg.arun_base + A.run_base;
+          i32 r = find_run(ar, A.run_cnt, seq[q]);
+          if (r >= 0) {
+            u32 order = ar[r].order + (seq[q] - ar[r].key);
+            u32 k = span_of_order(O, sg, O.canon_n[d], order);
+            if (k != INVALID) {
+              Span sp = O.canon[sg.canon_base + k];
+              ps = O.vpos[sg.canon_base + k] + (sp.len > 0 ? order - sp.order : 0u);
+              dl = sp.len < 0 ? 1 : 0;
+            }
+          }
+        }
+      }
+      pos[q] = ps;
+      deleted[q] = dl;
+    }
+    return;
+  }
+  constexpr u32 QPT = QBLK_Q / QBLK_T;
+  u32 od[QPT], kk[QPT];
+  // sweep 1: (agent, seq) -> order (the agent's item_orders runs)
+#pragma unroll
+  for (u32 j = 0; j < QPT; j++) {
+    u64 q = q0 + (u64)j * QBLK_T + t;
+    od[j] = INVALID;
+    if (q < q1) {
+      u32 a = agent[q], sq = seq[q];
+      if (a < st.n_agents) {
+        AgentRec A = P.agents[seg.agent_base + a];
+        const ARun* ar = P.arun + seg.arun_base + A.run_base;
+        i32 r = find_run(ar, A.run_cnt, sq);
+        if (r >= 0) od[j] = ar[r].order + (sq - ar[r].key);
+      }
+    }
+  }
+  // sweep 2: order -> span rank in LDS, rank -> span index (gathered together)
+#pragma unroll
+  for (u32 j = 0; j < QPT; j++) {
+    u32 o = od[j], wd = o >> 5;
+    u32 r = wd < used ? s_bw[QBLK_W + wd] + (u32)__popc(s_bw[wd] & (0xFFFFFFFFu >> (31u - (o & 31u)))) : 0u;
+    kk[j] = (o != INVALID && r != 0u && r <= cn) ? O.sorted[seg.canon_base + r - 1u] : INVALID;
+  }
+  // sweep 3: the span and its visible prefix
+#pragma unroll
+  for (u32 j = 0; j < QPT; j++) {
+    u64 q = q0 + (u64)j * QBLK_T + t;
+    if (q >= q1) break;
+    u32 ps = INVALID;
+    u8 dl = 2;
+    u32 k = kk[j];
+    if (k < cn) {
+      Span sp = O.canon[seg.canon_base + k];
+      u32 o = od[j];
+      if (o - sp.order < slen(sp)) {
+        ps = O.vpos[seg.canon_base + k] + (sp.len > 0 ? o - sp.order : 0u);
+        dl = sp.len < 0 ? 1 : 0;
+      }
+    }
+    pos[q] = ps;
+    deleted[q] = dl;
+  }
+}
+
 template <int L>
 __global__ void k_loc_to_pos(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* doc, const u16* agent, const u32* seq, u32* pos, u8* deleted) {
   for (u64 q = (u64)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (u64)gridDim.x * blockDim.x) {
