@@ -233,12 +233,15 @@ struct RangeSum {
 template <int L, bool WRITE, bool HASH = false>
 __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg, u32 ng, u32 a, u32 b, Span* canon,
                                               u32* vpos, u32* corder, u32 ccap, u32& out, u32& vis, u32 skip_first,
-                                              i32 extra, RangeSum& sum, u64& h) {
+                                              i32 extra, RangeSum& sum, u64& h, uint4* ring = nullptr) {
   const u32 l = lane_id();
   const Span* leaves = P.leaves + seg.leaf_base * L;
   const GroupRec* groups = P.groups + seg.grp_base;  // the root level, read in order from HBM
   const u32 vis0 = vis;
   u32 have = 0, skip = skip_first, nsp = 0, first_done = 0;
+  // HASH: spans are staged in this wave's 128-entry LDS ring as they are written and hashed 64 at a
+  // time (one digest evaluation per 64 spans instead of one per compaction step)
+  u32 hashed = out;
   Span open{0, 0, 0, 0};
   u32 open_vpos = 0;
   // the group holding leaf a: prefix of the groups' slot counts
@@ -316,7 +319,7 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
             else {
               if (l == 0u && out < ccap) {
                 canon[out] = open; vpos[out] = open_vpos; corder[out] = open.order;
-                if (HASH) h += span_hash(out, open);
+                if (HASH) ring[out & 127u] = make_uint4(open.order, open.ol, open.orr, (u32)open.len);
               }
               out++;
             }
@@ -333,7 +336,7 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
             canon[out + rank - sk] = sp;
             vpos[out + rank - sk] = vis + V - cl;
             corder[out + rank - sk] = v.x;
-            if (HASH) h += span_hash(out + rank - sk, sp);
+            if (HASH) ring[(out + rank - sk) & 127u] = make_uint4(sp.order, sp.ol, sp.orr, (u32)sp.len);
           }
           out += firsts - sk;
           if (sk) skip = 0;
@@ -345,6 +348,13 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
       }
       sum.last = Span{rdlane(v.x, nn - 1u), rdlane(v.y, nn - 1u), rdlane(v.z, nn - 1u), (i32)rdlane(v.w, nn - 1u)};
       vis += leaf_vis;
+      if (HASH) {  // every full block of 64 written spans: hashed from the ring, one span per lane
+        while (out - hashed >= 64u && hashed + 64u <= ccap) {
+          uint4 x = ring[(hashed + l) & 127u];
+          h += span_hash(hashed + l, Span{x.x, x.y, x.z, (i32)x.w});
+          hashed += 64u;
+        }
+      }
     }
     idx = base;
   }
@@ -355,9 +365,16 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
       open.len += extra;
       if (l == 0 && out < ccap) {
         canon[out] = open; vpos[out] = open_vpos; corder[out] = open.order;
-        if (HASH) h += span_hash(out, open);
+        if (HASH) ring[out & 127u] = make_uint4(open.order, open.ol, open.orr, (u32)open.len);
       }
       out++;
+    }
+  }
+  if (HASH) {  // the rest of the ring (< 128 spans)
+    u32 end = out < ccap ? out : ccap;
+    for (; hashed < end; hashed += 64u) {
+      uint4 x = ring[(hashed + l) & 127u];
+      if (hashed + l < end) h += span_hash(hashed + l, Span{x.x, x.y, x.z, (i32)x.w});
     }
   }
   sum.spans = nsp;
@@ -509,6 +526,7 @@ __device__ __forceinline__ u64 digest_counts(const DocState& s, u32 out) {
 // 8,192 documents in 1.33 rounds)
 template <int L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_publish(Pools P, PubOut O, u32 n, const u32* list, u32 xw) {
+  __shared__ uint4 s_ring[WAVES_PER_BLOCK][128];  // written spans awaiting the digest (compact_range)
   u32 d;
   if (!wave_doc(WAVES_PER_BLOCK, list, n, d)) return;
   WaveGPU<L> w;
@@ -525,7 +543,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   RangeSum sum{};
   u64 h = 0;
   compact_range<L, true, true>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, O.corder + seg.canon_base, seg.canon_cap,
-                               out, vis, 0u, 0, sum, h);
+                               out, vis, 0u, 0, sum, h, s_ring[threadIdx.x >> 6]);
   if (out > seg.canon_cap) {  // canonical spans beyond the planned capacity: report, never write past it
     if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
     return;
