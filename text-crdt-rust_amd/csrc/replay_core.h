@@ -1913,6 +1913,19 @@ struct Replayer {
         }
         if (pos >= rn) break;
         tried = kind == REC_RC ? 1u : 0u;
+      } else if (kind == REC_LC) {
+        // the same for compact local txns (local-trace corpora: configs 1 and 3)
+        while (true) {
+          u32 fast = fast_txn(pos, REC_LC, 0u, h, Rec{0, 0, 0, 0});
+          if (!fast) break;
+          pos += fast;
+          if (pos >= rn) break;
+          h = rec(pos);
+          kind = rec_kind(h);
+          if (kind != REC_LC) break;
+        }
+        if (pos >= rn) break;
+        tried = kind == REC_LC ? 1u : 0u;
       }
       u32 gen = opq(kind == REC_GEN ? 1u : 0u);
       Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
@@ -1936,7 +1949,6 @@ struct Replayer {
         // with record kind, format and stride known at compile time
         // (also the compact local form and generated ops: the other batch shapes)
         u32 fast = tried ? 0u
-                 : kind == REC_LC ? fast_txn(pos, REC_LC, 0u, h, gop)
                  : gen ? fast_txn(pos, REC_LTXN, 1u, h, gop) : fast_txn(pos, kind, 0u, h, gop);
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
