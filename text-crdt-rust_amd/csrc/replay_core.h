@@ -1740,7 +1740,9 @@ struct Replayer {
       u32 del = (r.w0 >> 27) & 1u;
       ins = del ^ 1u;
       u32 ra = r.w3 == 0xFFFFFFFFu ? ROOT_AGENT : agent;
-      o = del ? Rec{(REC_RDEL << 28) | l, agent, r.w2, 0u} : Rec{(REC_RINS << 28) | l, agent | (ra << 16), r.w2, r.w3};
+      // the op record as expand_rc's insert form; the delete paths read only its author (low half
+      // of w1) and target seq (w2), which the two forms share, so no per-field select
+      o = Rec{(REC_RINS << 28) | l, agent | (ra << 16), r.w2, r.w3};
       if (l == 0u) return 0;
       if (!fast_txn_ok(agent, seq, first)) return 0;
       if (r.w2 == 0xFFFFFFFFu) return 0;                   // origin_left / target ROOT
