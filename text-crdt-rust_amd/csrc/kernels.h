@@ -666,9 +666,17 @@ __global__ __launch_bounds__(PUBX_THREADS) void k_pub_index(Pools P, PubOut O, c
   u32* sorted = O.sorted + seg.canon_base;
   for (u32 i = t; i < used; i += PUBX_THREADS) lb[i] = 0u;
   __syncthreads();
-  for (u32 k = t; k < out; k += PUBX_THREADS) {
-    u32 o = co[k];
-    atomicOr(lb + (o >> 5), 1u << (o & 31u));
+  // (corder sweeps 8 loads per thread at a time: one dependent HBM wait per 8 spans, not per span)
+  for (u32 k0 = t; k0 < out; k0 += 8u * PUBX_THREADS) {
+    u32 ov[8];
+#pragma unroll
+    for (u32 u = 0; u < 8u; u++) {
+      u32 k = k0 + u * PUBX_THREADS;
+      ov[u] = k < out ? co[k] : INVALID;
+    }
+#pragma unroll
+    for (u32 u = 0; u < 8u; u++)
+      if (ov[u] != INVALID) atomicOr(lb + (ov[u] >> 5), 1u << (ov[u] & 31u));
   }
   __syncthreads();
   // group prefix: thread t owns groups [g0, g1)
@@ -694,12 +702,23 @@ __global__ __launch_bounds__(PUBX_THREADS) void k_pub_index(Pools P, PubOut O, c
     pre[i] = r;
   }
   // rank -> span
-  for (u32 k = t; k < out; k += PUBX_THREADS) {
-    u32 o = co[k], wd = o >> 5;
-    u32 r = lg[wd >> 3];
-    for (u32 j = wd & ~7u; j < wd; j++) r += (u32)__popc(lb[j]);
-    r += (u32)__popc(lb[wd] & ((1u << (o & 31u)) - 1u));
-    sorted[r] = k;
+  for (u32 k0 = t; k0 < out; k0 += 8u * PUBX_THREADS) {
+    u32 ov[8];
+#pragma unroll
+    for (u32 u = 0; u < 8u; u++) {
+      u32 k = k0 + u * PUBX_THREADS;
+      ov[u] = k < out ? co[k] : INVALID;
+    }
+#pragma unroll
+    for (u32 u = 0; u < 8u; u++) {
+      u32 o = ov[u];
+      if (o == INVALID) continue;
+      u32 wd = o >> 5;
+      u32 r = lg[wd >> 3];
+      for (u32 j = wd & ~7u; j < wd; j++) r += (u32)__popc(lb[j]);
+      r += (u32)__popc(lb[wd] & ((1u << (o & 31u)) - 1u));
+      sorted[r] = k0 + u * PUBX_THREADS;
+    }
   }
 }
 
