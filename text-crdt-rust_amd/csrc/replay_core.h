@@ -1450,25 +1450,24 @@ struct Replayer {
     }
     u32 k = 1, back = 0;
     u32 key = g(T_AGL_KEY);
-    do {  // a run of one-item deletes follows?  (early exits: see fast_txn_ok)
-      if (l != 1u) break;
-      if (b0 + 2u * per > nv) break;
-      if (remote) {
-        if ((o.w1 & 0xFFFFu) != agent) break;
-        if (o.w2 - key >= g(T_AGL_LEN)) break;
-      }
-      u32 delta;
-      if (cpt) {  // compact records: the next txn's target seq (RC w2) / pos (LC w1) read directly
-        Rec r2 = w.rec_get(b0 + per);
-        delta = remote ? r2.w2 - o.w2 : r2.w1 - o.w1;
-      } else {
-        Rec o2 = op_at(b0 + per, remote);
-        delta = remote ? o2.w2 - o.w2 : o2.w1 - o.w1;
-      }
-      back = opq(delta == 0xFFFFFFFFu ? 1u : 0u);
-      if (!back) {
-        if (delta != (remote ? 1u : 0u)) break;
-      }
+    // a run of one-item deletes follows?  The shape checks fold into one integer (one branch, so
+    // the two results have one merge), the next txn's target / pos read unconditionally (a window
+    // lane; ignored unless the checks pass)
+    u32 delta;
+    u32 has_next = b0 + 2u * per <= nv ? 1u : 0u;
+    u32 bn = has_next ? b0 + per : b0;  // (a valid window slot either way)
+    if (cpt) {  // compact records: the next txn's target seq (RC w2) / pos (LC w1) read directly
+      Rec r2 = w.rec_get(bn);
+      delta = remote ? r2.w2 - o.w2 : r2.w1 - o.w1;
+    } else {
+      Rec o2 = op_at(bn, remote);
+      delta = remote ? o2.w2 - o.w2 : o2.w1 - o.w1;
+    }
+    u32 bk = delta == 0xFFFFFFFFu ? 1u : 0u;
+    u32 bad = (l ^ 1u) | (has_next ^ 1u) | ((delta != (remote ? 1u : 0u) ? 1u : 0u) & (bk ^ 1u));
+    if (remote) bad |= ((o.w1 & 0xFFFFu) ^ agent) | (o.w2 - key >= g(T_AGL_LEN) ? 1u : 0u);
+    if (opq(bad) == 0u) {
+      back = opq(bk);
       {
         u32 room = back ? off + 1u : (u32)w.cget_len(idx) - off;  // targets stay in this entry
         if (remote) {  // ... and in the author's last item_orders run (contiguous orders)
@@ -1496,7 +1495,7 @@ struct Replayer {
 #endif
         k = k < room ? k : room;
       }
-    } while (0);
+    }
 #ifdef CRDT_PROF
 
 #endif
