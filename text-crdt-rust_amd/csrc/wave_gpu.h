@@ -478,9 +478,11 @@ struct WaveGPU {
         hl = Q;
         ok = X == ((REC_LC << 28) | agent) && Z == 0u && Q - 1u < 0xFFFFu && Y == p1 + p3;
       }
-      u64 stop = ballot(l > b0 && (!ok || l >= nv));
+      // lanes above b0 by a scalar mask (b0 < 64), the window end folded into the lane test, the
+      // run range as one unsigned compare: no lane-mask ANDs on the scalar unit
+      u64 stop = ballot(!ok || l >= nv) & (~1ull << b0);
       u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
-      total = wave_sum(l >= b0 && l < f ? hl : 0u);
+      total = wave_sum(l - b0 < f - b0 ? hl : 0u);
       return f - b0;
     }
     u32 rel = l - b0;  // wraps below b0: those lanes are masked
@@ -521,7 +523,7 @@ struct WaveGPU {
       u32 d = remote ? ((X ^ ((REC_RC << 28) | (1u << 27) | (1u << 16) | agent)) | (Y ^ (p1 + 1u)) | (Z ^ (p2 + delta)))
                      : ((X ^ ((REC_LC << 28) | agent)) | (Z ^ 1u) | Q | (Y ^ (p1 + delta)));
       bool ok = d == 0u;
-      u64 stop = ballot(l > b0 && (!ok || l >= nv));
+      u64 stop = ballot(!ok || l >= nv) & (~1ull << b0);
       u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
       return f - b0;
     }
