@@ -17,10 +17,11 @@ struct WaveCPU {
   WaveCPU() { std::memset(c, 0, sizeof(c)); std::memset(gb, 0, sizeof(gb)); std::memset(gc, 0, sizeof(gc)); std::memset(gv, 0, sizeof(gv)); }
 
   // context registers (plain array: slot f)
-  u32 x[128] = {};
+  u32 x[192] = {};
   u32 xg(u32 f) const { return x[f]; }
   template <class T> static T* gptr(u64 v) { return (T*)v; }
   void xs(u32 f, u32 v) { x[f] = v; }
+  void x_pin() {}
   void x_load_state(const DocState* p, u32 base) { std::memcpy(x + base, p, sizeof(DocState)); }
   void x_store_state(DocState* p, u32 base) const { std::memcpy(p, x + base, sizeof(DocState)); }
 

@@ -44,21 +44,34 @@ struct Cursor {
 };
 constexpr u32 END_LEAF = 0xFFFFFFFEu;  // memoised "no successor leaf"
 
-// Context slots (lane numbers of the two context VGPRs; < 64: first register).
+// Context slots: lane numbers of the three context VGPRs (f / 64 = the register).  x0 holds what
+// the replay never writes (table pointers, capacities), so writes to the others do not make the
+// compiler re-read it (a v_writelane defines a new value of its whole register); x1 DocState and
+// the per-call flags; x2 the leaf cache bookkeeping and the RLE tails.
 enum : u32 {
-  // table pointers, 2 slots each
+  // x0: table pointers, 2 slots each, and capacities (read-only while a document replays)
   P_LV = 0, P_DL = 2, P_DV = 4, P_SOL = 6, P_LOF = 8, P_CWO = 10, P_ARUN = 12, P_DELS = 14,
   P_DD = 16, P_TXNS = 18, P_PAR = 20, P_FR = 22, P_AGENTS = 24, P_GROUPS = 26, P_RECS = 28, P_STP = 30,
-  // capacities
-  K_LEAF = 32, K_MAP, K_CWO, K_TXN, K_DEL, K_DD, K_PAR, K_RECN,
-  // DocState, field for field (struct order, 20 dwords)
-  S_BASE = 40,
-  S_STATUS = 40, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
+  P_DDB = 32,             // (2 slots) double-delete block directory
+  P_PROBE = P_DDB + 2,    // (2 slots) probe answers
+  K_LEAF = P_PROBE + 2, K_MAP, K_CWO, K_TXN, K_DEL, K_DD, K_PAR, K_RECN,
+  K_FR,                   // frontier capacity
+  // x1: DocState, field for field (struct order), then the per-call flags
+  S_BASE = 64,
+  S_STATUS = 64, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
   S_N_DD, S_N_TXN, S_N_PAR, S_N_FR, S_N_AGENTS, S_N_ITEMS, S_CAP_NEED, S_N_ENTRIES, S_GEN_DONE, S_N_DDB,
   S_PROF0, S_PROF1, S_PROF2, S_PROF3,  // -DCRDT_PROF: cycles in typing / general / delete / insert paths
-  K_FR = 63,                            // frontier capacity
-  // leaf cache bookkeeping
-  C_LEAF = 64, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
+  // 1: the txn-level invariants fast_txn_ok checks hold (set by a fast commit, cleared by apply_txn)
+  F_FAST,
+  // a one-insert txn the fast path resolved but could not place (no free leaf for its split):
+  // flag, the item (4) and the cursor after its origin_left (3), handed to apply_txn.  Context
+  // lanes, not registers: this is the rare path, and registers live around the replay loop are
+  // what the 8-waves/SIMD budget spills.
+  F_PRE, PRE_ITEM, PRE_C = PRE_ITEM + 4,
+  F_GEN = PRE_C + 3,  // the record being replayed is a GEN record (generated ops)
+  T_RB_BASE,
+  // x2: leaf cache bookkeeping
+  C_LEAF = 128, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
   // RLE tails
   T_CWO_KEY, T_CWO_AGENT, T_CWO_SEQ, T_CWO_LEN,
@@ -67,22 +80,12 @@ enum : u32 {
   T_FR0,
   T_AG_ID, T_AG_BASE, T_AG_CNT, T_AG_CAP,
   T_AGL_KEY, T_AGL_ORDER, T_AGL_LEN,
-  T_RB_BASE,
-  P_DDB,  // (2 slots) double-delete block directory
-  P_PROBE = P_DDB + 2,  // (2 slots) probe answers
-  // 1: the txn-level invariants fast_txn_ok checks hold (set by a fast commit, cleared by apply_txn)
-  F_FAST = P_PROBE + 2,
-  // a one-insert txn the fast path resolved but could not place (no free leaf for its split):
-  // flag, the item (4) and the cursor after its origin_left (3), handed to apply_txn.  Context
-  // lanes, not registers: this is the rare path, and registers live around the replay loop are
-  // what the 8-waves/SIMD budget spills.
-  F_PRE, PRE_ITEM, PRE_C = PRE_ITEM + 4,
-  F_GEN = PRE_C + 3,  // the record being replayed is a GEN record (generated ops)
   N_SLOTS
 };
+static_assert(K_FR < 64, "read-only slots live in the first context register");
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
-static_assert(S_PROF3 < K_FR, "DocState lives in the first context register");
-static_assert(N_SLOTS <= 128, "two context registers");
+static_assert(T_RB_BASE < 128, "DocState and the flags live in the second context register");
+static_assert(N_SLOTS <= 192, "three context registers");
 
 template <class W, int L>
 struct Replayer {
@@ -1885,6 +1888,7 @@ struct Replayer {
     u32 pos = g(S_REC_POS);
     u32 rn = rec_n();
     while (pos < rn) {
+      w.x_pin();
       Rec h = rec(pos);
       u32 kind = rec_kind(h);
       u32 tried = 0;  // the fast path already declined this record
@@ -1908,6 +1912,7 @@ struct Replayer {
           if (!fast) break;
           pos += fast;
           if (pos >= rn) break;
+          w.x_pin();
           h = rec(pos);
           kind = rec_kind(h);
           if (kind != REC_RC) break;
@@ -1921,6 +1926,7 @@ struct Replayer {
           if (!fast) break;
           pos += fast;
           if (pos >= rn) break;
+          w.x_pin();
           h = rec(pos);
           kind = rec_kind(h);
           if (kind != REC_LC) break;

@@ -67,13 +67,19 @@ struct WaveGPU {
   // ---------------------------------------------------------------- context registers
   // Per-document scalar state, one field per lane (replay_core.h slot enum), accessed at
   // compile-time lane numbers: v_readlane / v_writelane, no memory, no SGPR pressure.
-  u32 x0 = 0, x1 = 0;
-  __device__ __forceinline__ u32 xg(u32 f) const { return f < 64 ? rdlane(x0, f) : rdlane(x1, f - 64); }
+  u32 x0 = 0, x1 = 0, x2 = 0;
+  __device__ __forceinline__ u32 xg(u32 f) const {
+    return f < 64 ? rdlane(x0, f) : f < 128 ? rdlane(x1, f - 64) : rdlane(x2, f - 128);
+  }
   __device__ __forceinline__ void xs(u32 f, u32 v) {  // v_writelane (no lane mask to keep live)
     u32 sv = uni(v);  // folds away for values the compiler already knows are uniform
     if (f < 64) x0 = wrlane(x0, sv, f);
-    else x1 = wrlane(x1, sv, f - 64);
+    else if (f < 128) x1 = wrlane(x1, sv, f - 64);
+    else x2 = wrlane(x2, sv, f - 128);
   }
+  // x0 (read-only in the replay) redefined opaquely once per replayed record: its reads are shared
+  // within a record's code but not hoisted out of the replay loop into long-lived SGPRs
+  __device__ __forceinline__ void x_pin() { asm volatile("" : "+v"(x0)); }
   // Element idx (x M) of a table, the byte offset computed in a VGPR: the compiler then addresses
   // it as table base (SGPR pair) + 32-bit VGPR offset -- one or two VALU ops -- instead of the
   // 64-bit SALU shift / add / add-with-carry chain a uniform index compiles to.  The replay is
@@ -94,18 +100,20 @@ struct WaveGPU {
     typedef __attribute__((address_space(1))) T GT;
     return (T*)(GT*)v;
   }
-  // DocState <-> slots [base, base + 20) of x0: one lane-parallel load / store
+  // DocState <-> the first lanes of x1 (slot base 64): one lane-parallel load / store
   __device__ __forceinline__ void x_load_state(const DocState* p, u32 base) {
+    (void)base;
     u32 l = lane();
     const u32* q = (const u32*)p;
-    bool mine = l >= base && l < base + (u32)(sizeof(DocState) / 4);
-    u32 v = q[mine ? l - base : 0u];  // clamped address: unconditional load, no exec branch
-    x0 = mine ? v : x0;
+    bool mine = l < (u32)(sizeof(DocState) / 4);
+    u32 v = q[mine ? l : 0u];  // clamped address: unconditional load, no exec branch
+    x1 = mine ? v : x1;
   }
   __device__ __forceinline__ void x_store_state(DocState* p, u32 base) const {
+    (void)base;
     u32 l = lane();
     u32* q = (u32*)p;
-    if (l >= base && l < base + (u32)(sizeof(DocState) / 4)) q[l - base] = x0;
+    if (l < (u32)(sizeof(DocState) / 4)) q[l] = x1;
   }
 
   __device__ __forceinline__ static u64 clock() { return __builtin_amdgcn_s_memtime(); }
