@@ -1507,8 +1507,7 @@ struct Replayer {
 #ifdef CRDT_PROF
     u64 pt1 = w.clock();
 #endif
-    // (one delete: leaf_delete directly; delete_segment's per-op checks hold by construction)
-    u32 done = split_first ? 0u : (k == 1u ? leaf_delete(idx, off, l) : delete_segment(idx, off, t1, k, back, l));
+    u32 done = split_first ? 0u : delete_segment(idx, off, t1, k, back, l);
 #ifdef CRDT_PROF
     u64 pt2 = w.clock();
 #endif
