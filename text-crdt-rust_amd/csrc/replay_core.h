@@ -377,8 +377,7 @@ struct Replayer {
   }
   CRDT_HD void ensure(u32 leaf) {
     if (leaf == g(C_LEAF)) return;
-    commit();
-    load_cache(leaf, w.ld_raw(w.at(sol(), leaf)));  // slot and entries: one round trip
+    load_cache(leaf, w.ld_raw(w.at(sol(), leaf)));  // (commits the cached leaf first) slot and entries: one round trip
   }
   // set entry idx of the cached leaf (tracks the cached visible count exactly)
   CRDT_HD void set(u32 idx, const Span& e) {
