@@ -16,6 +16,9 @@
  *   - A failing op poisons only its document (doc_status < 0); later ops of that document are
  *     skipped.  This mirrors "the reference panics": the document is dead, the rest live on.
  *   - Return value of every function: 0 = ok, < 0 = API error (CRDT_E_*).
+ *   - A stage / apply call names each document at most once (its docs[] has no duplicates);
+ *     a call that names a document twice returns CRDT_E_ARG and changes nothing.  Every stage
+ *     call replaces the staged streams of all documents (documents not named get none).
  */
 #ifndef CRDT_GPU_H
 #define CRDT_GPU_H

@@ -103,6 +103,8 @@ struct WaveCPU {
   void cset(u32 i, const Span& s) { c[i & 63] = s; }
   template <class F> void cset_lanes(u32 a, u32 b, F f) { for (u32 l = a; l < b && l < 64; l++) c[l] = f(l); }
   u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
+  u64 vis_lanes(u32 a, u32 b) const { u64 m = 0; for (u32 i = a; i < b && i < 64; i++) if (c[i].len > 0) m |= 1ull << i; return m; }
+  void negate_visible(u32 a, u32 b) { for (u32 i = a; i < b && i < 64; i++) if (c[i].len > 0) c[i].len = -c[i].len; }
   u64 lanes_in(u32 a, u32 b) const { u64 m = 0; for (u32 i = a; i < b && i < 64; i++) m |= 1ull << i; return m; }
   static u32 first_lane(u64 m) { return (u32)__builtin_ctzll(m); }
   i32 peek_find_order(const Span* p, u32 order, u32& start) const {

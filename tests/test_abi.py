@@ -34,3 +34,27 @@ def test_no_cpu_fallback():
         pytest.skip("GPU present")
     with pytest.raises(crdt_amd.CrdtError):
         crdt_amd.Engine(1)
+
+
+def test_codegen_guard_holds_for_the_built_library():
+    # build() refuses a library whose replay kernel leaves the 8-waves/SIMD register budget
+    # (<= 64 VGPRs, no scratch): the built one passes, at both leaf layouts
+    crdt_amd.build()
+    seen = crdt_amd.check_codegen(crdt_amd.LIB_PATH)
+    replay = [r for n, r in seen.items() if "8k_replayI" in n]
+    assert len(replay) == 2
+    for r in replay:
+        assert r["vgpr_count"] <= 64 and r.get("private_segment_fixed_size", 0) == 0
+
+
+def test_codegen_guard_rejects_a_bloated_kernel(monkeypatch):
+    res = crdt_amd.kernel_resources(crdt_amd.LIB_PATH)
+    name = next(n for n in res if "8k_replayILi32E" in n)
+    bad = dict(res)
+    bad[name] = dict(res[name], vgpr_count=97)
+    monkeypatch.setattr(crdt_amd, "kernel_resources", lambda p: bad)
+    with pytest.raises(crdt_amd.CrdtError, match="vgpr_count = 97"):
+        crdt_amd.check_codegen(crdt_amd.LIB_PATH)
+    bad[name] = dict(res[name], private_segment_fixed_size=16)
+    with pytest.raises(crdt_amd.CrdtError, match="private_segment_fixed_size"):
+        crdt_amd.check_codegen(crdt_amd.LIB_PATH)

@@ -57,8 +57,72 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defin
     r = subprocess.run(cmd, capture_output=not verbose, text=True)
     if r.returncode != 0:
         raise CrdtError("hipcc failed:\n" + (r.stderr or "")[-4000:])
+    check_codegen(out + ".tmp")
     os.replace(out + ".tmp", out)
     return out
+
+
+# The replay's speed rests on its register budget: 8 waves per SIMD need <= 64 VGPRs (the 512-
+# VGPR file / 8), and a scratch spill would put HBM round trips into every context access.  A
+# toolchain change that breaks either would silently halve throughput (97 VGPRs =
+# 4 waves/SIMD = 216 ms vs 185 ms), so build() refuses such a library.
+CODEGEN_LIMITS = {
+    "k_replay": {"vgpr_count": 64, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
+    "k_publish": {"vgpr_count": 64, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
+}
+LLVM_BIN = "/opt/rocm/lib/llvm/bin"
+
+
+def kernel_resources(lib_path: str) -> dict:
+    """Per-kernel resource metadata of the gfx950 code object inside `lib_path` (the AMDGPU
+    metadata note: .vgpr_count, .sgpr_count, spills, .private_segment_fixed_size, LDS)."""
+    import re
+    import tempfile
+    import shutil
+    with tempfile.TemporaryDirectory() as td:
+        # the HIP fat binary sits in the library's .hip_fatbin section; llvm-objdump --offloading
+        # extracts its bundles next to the (copied) input
+        cp = os.path.join(td, "lib.so")
+        shutil.copyfile(lib_path, cp)
+        r = subprocess.run([os.path.join(LLVM_BIN, "llvm-objdump"), "--offloading", cp], capture_output=True, text=True)
+        cos = [f for f in os.listdir(td) if "amdgcn-amd-amdhsa--gfx950" in f]
+        if r.returncode != 0 or not cos:
+            raise CrdtError("no gfx950 code object in " + lib_path + ": " + (r.stderr or "")[-500:])
+        notes = subprocess.run([os.path.join(LLVM_BIN, "llvm-readelf"), "--notes", os.path.join(td, cos[0])],
+                               capture_output=True, text=True, check=True).stdout
+    out, cur = {}, {}
+    for line in notes.splitlines():
+        m = re.match(r"\s*-?\s*\.(\w+):\s+(\S+)\s*$", line)
+        if not m:
+            continue
+        k, v = m.group(1), m.group(2)
+        if line.lstrip().startswith("- "):
+            cur = {}
+        if k == "name":
+            out[v] = cur
+        elif re.fullmatch(r"-?\d+", v):
+            cur[k] = int(v)
+    return out
+
+
+def check_codegen(lib_path: str) -> dict:
+    """Raise CrdtError if a guarded kernel exceeds CODEGEN_LIMITS; returns the guarded kernels'
+    resources."""
+    res = kernel_resources(lib_path)
+    seen = {}
+    for name, r in res.items():
+        for k, lim in CODEGEN_LIMITS.items():
+            if f"{len(k)}{k}I" not in name:  # mangled template name, e.g. _ZN4crdt8k_replayILi32EE...
+                continue
+            seen[name] = r
+            for field, mx in lim.items():
+                if r.get(field, 0) > mx:
+                    raise CrdtError(f"codegen guard: {name} {field} = {r.get(field)} > {mx} "
+                                    f"(the replay's 8-waves/SIMD register budget; see DESIGN.md §4)")
+    for k in CODEGEN_LIMITS:
+        if not any(f"{len(k)}{k}I" in n for n in seen):
+            raise CrdtError(f"codegen guard: kernel {k} not found in {lib_path}")
+    return seen
 
 
 _lib = None

@@ -562,6 +562,13 @@ struct crdt_engine {
       probe_cap = total;
       HIPCHK(dalloc(probe, probe_cap));
     }
+    if (has_probes) {
+      // every probe slot starts as the "unknown" answer: probes after a document's stop point
+      // never run, and must not report a previous call's (or uninitialised) answers
+      std::vector<uint4> unk(total, make_uint4(0xFFFFu, INVALID, INVALID, 2u));
+      HIPCHK(hipMemcpyAsync(probe, unk.data(), total * sizeof(uint4), hipMemcpyHostToDevice, stream));
+      HIPCHK(hipStreamSynchronize(stream));
+    }
     for (auto& sg : seg_h) { sg.rec_base = 0; sg.rec_n = 0; }
     // Consecutive distinct streams go up in one host->device copy; a replicated stream (same
     // host vector as the previous document) is a device-to-device copy of that upload.
@@ -982,7 +989,8 @@ int crdt_agent_intern_dev(crdt_engine* e, uint64_t n, const uint32_t* doc, const
                           const char* bytes, uint16_t* out, uint32_t* rank_out) {
   if (!valid(e) || (n && (!doc || !name_off || !bytes || !out))) return CRDT_E_ARG;
   if (!n) return 0;
-  std::vector<u32> group_of_doc;  // doc -> group + 1 (sparse via map for large engines)
+  int rs = e->set_device();  // (scratch and the launch belong on the engine's device)
+  if (rs) return rs;
   std::unordered_map<u32, u32> gmap;
   std::vector<u32> gdoc;
   std::vector<std::vector<u64>> grefs;  // per group: call refs (indices into the call)

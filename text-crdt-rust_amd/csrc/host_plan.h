@@ -274,7 +274,10 @@ inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_
   // fills stops its document resumably and grows)
   c.del = (u32)std::min<u64>(std::min<u64>(nd.local_del + nd.remote_del_ops, 2 * (nd.local_del_ops + nd.remote_del_ops) + 64) + 1,
                              0xFFFFFFFFull);
-  c.dd = nd.remote_del_ops ? 4u : 0u;  // double-delete blocks: grown on demand (rare but for config 5)
+  // double-delete blocks: grown on demand (rare but for config 5).  fits() reserves
+  // (4 * entries + 2 * txn_len + 2) / 32 + 2 blocks before a remote delete txn, so the first
+  // capacity covers the stream's longest txn on an empty table: no relaunch just for its reserve.
+  c.dd = nd.remote_del_ops ? std::max<u32>(4u, (u32)std::min<u64>((2ull * nd.max_len + 2) / 32 + 3, 0x7FFFFFFFull)) : 0u;
   c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + 64 + 1, 1024 + (nd.remote_parents + nd.n_txn) / 64);
   c.agent = n_agents;
   return c;

@@ -1674,6 +1674,7 @@ struct Replayer {
     Span e = w.cget(idx);
     u32 n = g(C_N);
     u32 len = (u32)item.len;
+    if (off == 0u) return leaf_insert_front(item);  // (idx == 0: the front of the document)
     u32 has_rem = off < slen(e);
     u32 space = 1u + has_rem;
     if (n + space > (u32)L) return 0;
@@ -1695,6 +1696,115 @@ struct Replayer {
     p(C_NOW, g(C_NOW) + len);
     p(C_DIRTY, 1u);
     inc(S_N_ITEMS, len);
+    return 1;
+  }
+  // The item as entry 0 of the cached first leaf (cursor at the start of the document, offset 0 at
+  // index 0: insert_internal neither rolls back nor splits, mutations.rs:34-52) without a leaf split.
+  CRDT_HD u32 leaf_insert_front(const Span& item) {
+    u32 n = g(C_N);
+    u32 len = (u32)item.len;
+    if (n + 1u > (u32)L) return 0;
+    if (g(K_MAP) - item.order < len) return 0;
+    w.cache_shift_right(0u, n, 1u);
+    p(C_N, n + 1u);
+    inc(S_N_ENTRIES, 1u);
+    map_fill(item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
+    w.cset(0u, item);
+    p(C_NOW, g(C_NOW) + len);
+    p(C_DIRTY, 1u);
+    inc(S_N_ITEMS, len);
+    return 1;
+  }
+  // A local delete of l visible items that starts at offset `off` of visible entry idx of the
+  // cached leaf and runs past that entry (rem: the visible position of its first item within the
+  // leaf).  local_deactivate (mutations.rs:520-570) visits the entries in order, skipping deleted
+  // ones, and mutate_entry (:227-277) deactivates each visible one:
+  //  * entry idx: in place from offset 0, else [E[..off]] then the deleted rest d0, which
+  //    insert_internal (:17-179) prepends onto the entry after idx when that one is a deleted run
+  //    d0 can append to (a visible entry cannot take it), else inserts at idx + 1;
+  //  * every visible entry up to the last one: in place (the delete continues past it);
+  //  * the last entry kl: in place when the delete ends at its end, else [its deleted head] then
+  //    the visible rest c, prepended onto the entry after kl or inserted there.
+  // The deletes log gets one append per deactivated piece, in document order (doc.rs:414-426).
+  // Conditions are evaluated on the leaf as the reference's order of steps sees it: the entry
+  // after idx is untouched when d0 goes in, the entry after kl when c goes in.  Returns 0, having
+  // changed nothing, when the delete leaves the leaf or the leaf has no room (the general path
+  // then splits it).
+  CRDT_HD u32 leaf_delete_span(u32 idx, u32 off, u32 l, u32 rem, u32 first) {
+    u32 n = g(C_N);
+    u32 kl, ol;
+    if (!w.cfind_content(n, rem + l - 1u, kl, ol)) return 0;
+    if (kl >= n) return 0;
+    if (g(K_DEL) - g(S_N_DEL) < l) return 0;  // (one delete run per deactivated piece at most)
+    if (g(K_MAP) - first < l) return 0;
+    Span E = w.cget(idx), Z = w.cget(kl);
+    u32 rl = ol + 1u;  // items deleted from entry kl
+    u32 has_c = rl < (u32)Z.len ? 1u : 0u;
+    Span cc{Z.order + rl, Z.order + rl - 1u, Z.orr, Z.len - (i32)rl};
+    Span nx{0, 0, 0, 0};
+    u32 c_pre = 0u;
+    if (has_c) {
+      if (kl + 1u < n) {
+        nx = w.cget(kl + 1u);
+        c_pre = can_append_u(cc, nx) ? 1u : 0u;
+      }
+    }
+    u32 has_a = off > 0u ? 1u : 0u;
+    Span d0{E.order + off, E.order + off - 1u, E.orr, -(E.len - (i32)off)};
+    Span n1{0, 0, 0, 0};
+    u32 d_pre = 0u;
+    if (has_a) {
+      n1 = w.cget(idx + 1u);  // (idx < kl < n)
+      d_pre = can_append_u(d0, n1) ? 1u : 0u;
+    }
+    u32 add = (has_a & (d_pre ^ 1u)) + (has_c & (c_pre ^ 1u));
+    if (n + add > (u32)L) return 0;
+    // deletes log: the pieces in document order (entries idx .. kl as they are now)
+    u32 key = first;
+    append_delete(key, d0.order, (u32)E.len - off);
+    key += (u32)E.len - off;
+    for (u64 m = w.vis_lanes(idx + 1u, kl); m; m &= m - 1ull) {
+      u32 j = W::first_lane(m);
+      u32 o = w.cget_order(j), ln = (u32)w.cget_len(j);
+      append_delete(key, o, ln);
+      key += ln;
+    }
+    append_delete(key, Z.order, rl);
+    // the leaf, from the right end (so that earlier indices stay put)
+    Z.len = -(i32)rl;
+    w.cset(kl, Z);
+    if (has_c) {
+      if (c_pre) {
+        nx.order = cc.order;  // YjsSpan::prepend keeps origin_left (span.rs:61-64)
+        nx.len += cc.len;
+        w.cset(kl + 1u, nx);
+      } else {
+        w.cache_shift_right(kl + 1u, n, 1u);
+        w.cset(kl + 1u, cc);
+        n += 1u;
+      }
+    }
+    w.negate_visible(idx + 1u, kl);  // the entries strictly between idx and kl
+    if (has_a) {
+      w.cset(idx, Span{E.order, E.ol, E.orr, (i32)off});
+      if (d_pre) {
+        n1.order = d0.order;
+        n1.len += d0.len;
+        w.cset(idx + 1u, n1);
+      } else {
+        w.cache_shift_right(idx + 1u, n, 1u);
+        w.cset(idx + 1u, d0);
+        n += 1u;
+      }
+    } else {
+      E.len = -E.len;
+      w.cset(idx, E);
+    }
+    p(C_N, n);
+    inc(S_N_ENTRIES, add);
+    p(C_NOW, g(C_NOW) - l);
+    p(C_DIRTY, 1u);
+    fast_txn_commit(first, l);
     return 1;
   }
   // Returns the records consumed by a fast-path txn at `pos`, or 0 (use apply_txn).
@@ -1783,17 +1893,31 @@ struct Replayer {
       l = del + o.w3;
       if ((del != 0u) == ins) return 0;
       if (l - 1u >= 0xFFFFu) return 0;
-      if (ins) {
-        if (lp == 0u) return 0;
-      }
       if (gen_form) {
         u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l);
         if (!ok) return 0;
       }
       if (!fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first)) return 0;
-      if (!cursor_at_content_pos(ins ? lp - 1u : lp, c)) return 0;  // root.rs:54-88 (loads the leaf)
-      ol = w.cget_order(c.idx) + c.off;  // doc.rs:446-449: the item at pos - 1, then Cursor::next
-      c.off += ins;
+      if (ins && lp == 0u) {
+        // doc.rs:443-444: origin_left ROOT, the cursor at the start of the document (root.rs:133-
+        // 150); integrate stops at once (origin_right is the item there) and insert_internal puts
+        // the item before entry 0 (offset 0 at index 0: nothing to append to)
+        c = cursor_at_start();
+        ensure(c.leaf);
+        p(C_VSTART, 0u);  // (the first leaf starts at visible position 0)
+        p(C_VS_OK, 1u);
+        ol = ROOT_ORDER;
+      } else {
+        if (!cursor_at_content_pos(ins ? lp - 1u : lp, c)) return 0;  // root.rs:54-88 (loads the leaf)
+        ol = w.cget_order(c.idx) + c.off;  // doc.rs:446-449: the item at pos - 1, then Cursor::next
+        c.off += ins;
+        if (!ins) {
+          // a delete that runs past its first entry (local_deactivate over several entries of
+          // the cached leaf): the multi-entry form, when it stays in the leaf
+          i32 el = w.cget_len(c.idx);
+          if (el > 0 && c.off + l > (u32)el) return leaf_delete_span(c.idx, c.off, l, lp - g(C_VSTART), first) ? per : 0u;
+        }
+      }
     }
     u32 idx = c.idx;
     if (ins) {
@@ -1932,6 +2056,18 @@ struct Replayer {
         }
         if (pos >= rn) break;
         tried = kind == REC_LC ? 1u : 0u;
+      } else if (kind == REC_GEN) {
+        // generated ops (config 4) in a loop of their own: gen_op and one fast-path instance per
+        // op, no trip through the record window and the kind dispatch
+        u32 done = g(S_GEN_DONE), n_gen = h.w2;
+        while (done < n_gen) {
+          Rec go = gen_op(h.w3, done, cur_len());
+          Rec gh{(REC_LTXN << 28) | 1u, h.w1, go.w2, go.w2 + go.w3};
+          if (!fast_txn(pos, REC_LTXN, 1u, gh, go)) break;
+          done++;
+        }
+        p(S_GEN_DONE, done);
+        tried = 1u;  // (the general path takes op `done`, or the record ends below)
       }
       u32 gen = opq(kind == REC_GEN ? 1u : 0u);
       Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
@@ -1954,8 +2090,7 @@ struct Replayer {
         // compact remote txns (the remote-batch hot path) get their own instance of the fast paths,
         // with record kind, format and stride known at compile time
         // (also the compact local form and generated ops: the other batch shapes)
-        u32 fast = tried ? 0u
-                 : gen ? fast_txn(pos, REC_LTXN, 1u, h, gop) : fast_txn(pos, kind, 0u, h, gop);
+        u32 fast = tried ? 0u : fast_txn(pos, kind, 0u, h, gop);  // (a GEN record was tried above)
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
         u32 dt = prof_mode == 0u ? (u32)(t1 - t0) : prof_mode == 1u ? 1u : (fast ? fast / per_txn(kind == REC_RTXN || kind == REC_RC) : 0u);

@@ -319,6 +319,13 @@ struct WaveGPU {
     er = in ? s.orr : er;
     en = in ? s.len : en;
   }
+  // the visible entries among lanes [a, b), as a lane mask
+  __device__ __forceinline__ u64 vis_lanes(u32 a, u32 b) const { u32 l = lane(); return ballot(l >= a && l < b && en > 0); }
+  // deactivate (negate) the visible entries among lanes [a, b)
+  __device__ __forceinline__ void negate_visible(u32 a, u32 b) {
+    u32 l = lane();
+    en = (l >= a && l < b && en > 0) ? -en : en;
+  }
   // lanes [a, b) as a mask, and the lowest lane of a mask (wave-uniform)
   __device__ __forceinline__ u64 lanes_in(u32 a, u32 b) const { u32 l = lane(); return ballot(l >= a && l < b); }
   __device__ __forceinline__ static u32 first_lane(u64 m) { return (u32)__builtin_ctzll(m); }
