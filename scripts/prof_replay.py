@@ -17,9 +17,12 @@ ap.add_argument("--trace", default="automerge-paper")
 ap.add_argument("--local", action="store_true")
 ap.add_argument("--wire", default=None, help="a .rtx.gz remote wire file instead of a trace")
 ap.add_argument("--clean", action="store_true", help="reset and replay once more (single launch)")
+ap.add_argument("--random", type=int, default=0, help="config 4: this many generated ops per document")
 a = ap.parse_args()
 e = crdt_amd.Engine(a.docs, 32)
-if a.local:
+if a.random:
+    e.stage_random(list(range(a.docs)), "gen", a.random, 0xC0FFEE)
+elif a.local:
     t = load_trace(a.trace)
     ag = e.agent_intern(list(range(a.docs)), ["jeremy"] * a.docs)
     e.apply_trace(list(range(a.docs)), int(ag[0]), t.counts, t.patches, stage_only=True)

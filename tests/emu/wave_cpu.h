@@ -156,6 +156,9 @@ struct WaveCPU {
     for (u32 i = 0; i < n_ahead; i++) qb[i] = p_ahead[i];
   }
   Rec rec_get(u32 k) const { return rb[k]; }
+  void gen_draws(u32 seed, u32 base) {
+    for (u32 i = 0; i < 64; i++) { GenDraw d = gen_draw(seed, base + i); rb[i] = Rec{d.hi, d.lo, d.r2, 0u}; }
+  }
   // the GPU backend's scans over 64 records at p (no window move); len0 = the first txn's length
   u32 typing_scan_at(const Rec* p, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3, u32& total, u32& len0) const {
     Rec t[64];

@@ -173,15 +173,24 @@ CRDT_HD u64 mix64(u64 z) {  // splitmix64 finaliser
 // U[0, len - 1].  The reference's SmallRng stream is Rust-only, so draws come from a counter-based
 // hash of (seed, op#) with fixed-point thresholds: integer-exact on the device and in the oracle.
 // Returns the LOP record of op `i` for a document of visible length `len`.
-CRDT_HD Rec gen_op(u32 seed, u32 i, u32 len) {
+// The draws of op i: r = mix64(seed << 32 | i) (hi, lo halves) and r2 = low half of mix64(r).
+// They do not depend on the document, so the replay computes 64 ops' draws lane-parallel.
+struct GenDraw { u32 hi, lo, r2; };
+CRDT_HD GenDraw gen_draw(u32 seed, u32 i) {
   u64 r = mix64(((u64)seed << 32) | i);
-  u32 hi = (u32)(r >> 32), lo = (u32)r;
+  return GenDraw{(u32)(r >> 32), (u32)r, (u32)mix64(r)};
+}
+// The LocalOp of a draw for a document of visible length len.
+CRDT_HD Rec gen_op_of(u32 hi, u32 lo, u32 r2, u32 len) {
   u32 thr = len < 100u ? 0x8CCCCCCDu : 0x73333333u;  // 0.55 / 0.45 of 2^32
   if (len == 0u || hi < thr) return Rec{REC_LOP << 28, (u32)(((u64)lo * (len + 1u)) >> 32), 0u, 1u};
   u32 p = (u32)(((u64)lo * len) >> 32);
   u32 mx = len - p < 10u ? len - p : 10u;
-  u32 r2 = (u32)mix64(r);
   return Rec{REC_LOP << 28, p, 1u + (u32)(((u64)r2 * mx) >> 32), 0u};
+}
+CRDT_HD Rec gen_op(u32 seed, u32 i, u32 len) {
+  GenDraw d = gen_draw(seed, i);
+  return gen_op_of(d.hi, d.lo, d.r2, len);
 }
 
 // ---------------------------------------------------------------------------------------------

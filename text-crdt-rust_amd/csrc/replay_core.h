@@ -1670,11 +1670,12 @@ struct Replayer {
   // stops at once and the run cannot be appended: insert_internal (mutations.rs:17-179) splits
   // the entry at the cursor (remainder after the item) and makes room, without a leaf split.
   // Returns 0, having changed nothing, when the leaf or the order map has no room.
-  CRDT_HD u32 leaf_insert(u32 idx, u32 off, const Span& item) {
+  // front: the cursor is at offset 0 of entry 0 (a local insert at position 0; never remote)
+  CRDT_HD u32 leaf_insert(u32 idx, u32 off, const Span& item, u32 front) {
+    if (front) return leaf_insert_front(item);
     Span e = w.cget(idx);
     u32 n = g(C_N);
     u32 len = (u32)item.len;
-    if (off == 0u) return leaf_insert_front(item);  // (idx == 0: the front of the document)
     u32 has_rem = off < slen(e);
     u32 space = 1u + has_rem;
     if (n + space > (u32)L) return 0;
@@ -1731,74 +1732,81 @@ struct Replayer {
   // changed nothing, when the delete leaves the leaf or the leaf has no room (the general path
   // then splits it).
   CRDT_HD u32 leaf_delete_span(u32 idx, u32 off, u32 l, u32 rem, u32 first) {
+    // (few scalars live at a time, entries re-read from the cache where they are written: this
+    // path shares the replay's register budget with the hot loops)
     u32 n = g(C_N);
     u32 kl, ol;
     if (!w.cfind_content(n, rem + l - 1u, kl, ol)) return 0;
     if (kl >= n) return 0;
     if (g(K_DEL) - g(S_N_DEL) < l) return 0;  // (one delete run per deactivated piece at most)
     if (g(K_MAP) - first < l) return 0;
-    Span E = w.cget(idx), Z = w.cget(kl);
     u32 rl = ol + 1u;  // items deleted from entry kl
-    u32 has_c = rl < (u32)Z.len ? 1u : 0u;
-    Span cc{Z.order + rl, Z.order + rl - 1u, Z.orr, Z.len - (i32)rl};
-    Span nx{0, 0, 0, 0};
-    u32 c_pre = 0u;
-    if (has_c) {
-      if (kl + 1u < n) {
-        nx = w.cget(kl + 1u);
-        c_pre = can_append_u(cc, nx) ? 1u : 0u;
+    // the pieces insert_internal places, and whether each prepends onto the entry after it
+    u32 c_add = 0u, c_pre = 0u;
+    {
+      Span Z = w.cget(kl);
+      if (rl < (u32)Z.len) {
+        c_add = 1u;
+        if (kl + 1u < n) c_pre = can_append_u(Span{Z.order + rl, Z.order + rl - 1u, Z.orr, Z.len - (i32)rl}, w.cget(kl + 1u)) ? 1u : 0u;
       }
     }
-    u32 has_a = off > 0u ? 1u : 0u;
-    Span d0{E.order + off, E.order + off - 1u, E.orr, -(E.len - (i32)off)};
-    Span n1{0, 0, 0, 0};
-    u32 d_pre = 0u;
-    if (has_a) {
-      n1 = w.cget(idx + 1u);  // (idx < kl < n)
-      d_pre = can_append_u(d0, n1) ? 1u : 0u;
+    u32 d_add = 0u, d_pre = 0u;
+    if (off) {
+      Span E = w.cget(idx);
+      d_add = 1u;
+      d_pre = can_append_u(Span{E.order + off, E.order + off - 1u, E.orr, (i32)off - E.len}, w.cget(idx + 1u)) ? 1u : 0u;  // (idx < kl < n)
     }
-    u32 add = (has_a & (d_pre ^ 1u)) + (has_c & (c_pre ^ 1u));
+    u32 add = (d_add & (d_pre ^ 1u)) + (c_add & (c_pre ^ 1u));
     if (n + add > (u32)L) return 0;
-    // deletes log: the pieces in document order (entries idx .. kl as they are now)
+    // deletes log: the deactivated pieces in document order (entries idx .. kl as they are now)
     u32 key = first;
-    append_delete(key, d0.order, (u32)E.len - off);
-    key += (u32)E.len - off;
-    for (u64 m = w.vis_lanes(idx + 1u, kl); m; m &= m - 1ull) {
+    for (u64 m = w.vis_lanes(idx, kl + 1u); m; m &= m - 1ull) {
       u32 j = W::first_lane(m);
-      u32 o = w.cget_order(j), ln = (u32)w.cget_len(j);
-      append_delete(key, o, ln);
+      u32 s0 = j == idx ? off : 0u;
+      u32 ln = (j == kl ? rl : (u32)w.cget_len(j)) - s0;
+      append_delete(key, w.cget_order(j) + s0, ln);
       key += ln;
     }
-    append_delete(key, Z.order, rl);
     // the leaf, from the right end (so that earlier indices stay put)
-    Z.len = -(i32)rl;
-    w.cset(kl, Z);
-    if (has_c) {
-      if (c_pre) {
-        nx.order = cc.order;  // YjsSpan::prepend keeps origin_left (span.rs:61-64)
-        nx.len += cc.len;
-        w.cset(kl + 1u, nx);
-      } else {
-        w.cache_shift_right(kl + 1u, n, 1u);
-        w.cset(kl + 1u, cc);
-        n += 1u;
+    {
+      Span Z = w.cget(kl);
+      Span cc{Z.order + rl, Z.order + rl - 1u, Z.orr, Z.len - (i32)rl};
+      Z.len = -(i32)rl;
+      w.cset(kl, Z);
+      if (c_add) {
+        if (c_pre) {
+          Span nx = w.cget(kl + 1u);
+          nx.order = cc.order;  // YjsSpan::prepend keeps origin_left (span.rs:61-64)
+          nx.len += cc.len;
+          w.cset(kl + 1u, nx);
+        } else {
+          w.cache_shift_right(kl + 1u, n, 1u);
+          w.cset(kl + 1u, cc);
+          n += 1u;
+        }
       }
     }
     w.negate_visible(idx + 1u, kl);  // the entries strictly between idx and kl
-    if (has_a) {
-      w.cset(idx, Span{E.order, E.ol, E.orr, (i32)off});
-      if (d_pre) {
-        n1.order = d0.order;
-        n1.len += d0.len;
-        w.cset(idx + 1u, n1);
+    {
+      Span E = w.cget(idx);
+      if (d_add) {
+        Span d0{E.order + off, E.order + off - 1u, E.orr, (i32)off - E.len};
+        E.len = (i32)off;
+        w.cset(idx, E);
+        if (d_pre) {
+          Span n1 = w.cget(idx + 1u);
+          n1.order = d0.order;
+          n1.len += d0.len;
+          w.cset(idx + 1u, n1);
+        } else {
+          w.cache_shift_right(idx + 1u, n, 1u);
+          w.cset(idx + 1u, d0);
+          n += 1u;
+        }
       } else {
-        w.cache_shift_right(idx + 1u, n, 1u);
-        w.cset(idx + 1u, d0);
-        n += 1u;
+        E.len = -E.len;
+        w.cset(idx, E);
       }
-    } else {
-      E.len = -E.len;
-      w.cset(idx, E);
     }
     p(C_N, n);
     inc(S_N_ENTRIES, add);
@@ -1958,7 +1966,7 @@ struct Replayer {
       u32 total;
       u32 nt = typing_run(b0, nv, remote, agent, (agent & 0xFFFFu) | (o.w1 & 0xFFFF0000u), o, total);
       item.len = (i32)total;
-      if (!leaf_insert(idx, c.off, item)) return 0;
+      if (!leaf_insert(idx, c.off, item, remote ? 0u : (c.off == 0u ? 1u : 0u))) return 0;
       fast_txn_commit(first, total);
       return nt * per;
     }
@@ -1968,6 +1976,18 @@ struct Replayer {
 #ifdef CRDT_PROF
     prof_cat = 2u;
 #endif
+    if (gen) {  // a generated op starts no run (no window): one leaf_delete when the leaf has room
+      u32 t1 = w.cget_order(idx) + c.off;
+      if (g(K_MAP) - first >= l) {
+        if (g(K_DEL) != g(S_N_DEL)) {
+          if (leaf_delete(idx, c.off, l)) {
+            append_delete(first, t1, l);  // doc.rs:414-426
+            fast_txn_commit(first, l);
+            return per;
+          }
+        }
+      }
+    }
     return fast_deletes(b0, nv, remote, agent, idx, c.off, l, first, o);
   }
 
@@ -2059,9 +2079,19 @@ struct Replayer {
       } else if (kind == REC_GEN) {
         // generated ops (config 4) in a loop of their own: gen_op and one fast-path instance per
         // op, no trip through the record window and the kind dispatch
+        // The draws of 64 ops at a time are computed lane-parallel into the record window's
+        // registers (the window is reloaded at the next record: T_RB_BASE invalid).
         u32 done = g(S_GEN_DONE), n_gen = h.w2;
+        p(T_RB_BASE, 0x80000000u);
+        u32 base = done;
+        w.gen_draws(h.w3, base);
         while (done < n_gen) {
-          Rec go = gen_op(h.w3, done, cur_len());
+          if (done - base >= 64u) {
+            base = done;
+            w.gen_draws(h.w3, base);
+          }
+          Rec d = w.rec_get(done - base);
+          Rec go = gen_op_of(d.w0, d.w1, d.w2, cur_len());
           Rec gh{(REC_LTXN << 28) | 1u, h.w1, go.w2, go.w2 + go.w3};
           if (!fast_txn(pos, REC_LTXN, 1u, gh, go)) break;
           done++;

@@ -466,6 +466,13 @@ struct WaveGPU {
   __device__ __forceinline__ Rec rec_get(u32 k) const {
     return Rec{rdlane(rx, k), rdlane(ry, k), rdlane(rz, k), rdlane(rw, k)};
   }
+  // The generator draws of ops [base, base + 64) into the window registers (lane k: hi, lo, r2 of
+  // op base + k), computed lane-parallel on the vector unit; read back with rec_get.  (A GEN record
+  // uses no record window: the replay invalidates the window while it runs one.)
+  __device__ __forceinline__ void gen_draws(u32 seed, u32 base) {
+    GenDraw d = gen_draw(seed, base + lane());
+    rx = d.hi; ry = d.lo; rz = d.r2;
+  }
   // Typing-run scan (replay_core.h fast_typing): lane k checks record k of the prefetch block
   // against "txn continues the typing txn before it" -- remote: RTXN{1 op, 1 parent}, RINS with
   // origin_left = (agent, seq-1) and the same origin_right, RPARENT (agent, seq-1), seq = previous
