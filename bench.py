@@ -215,14 +215,22 @@ def golden(trace: str, key: str):
         return None
 
 
+TRAFFIC_WORKLOAD = {"k_replay": "automerge-paper remote, one clean launch",
+                    "k_materialize": "automerge-paper remote, per-document content copies, one launch"}
+
+
 def measured_traffic(n_docs: int, kernel: str = "k_replay"):
     """HBM bytes per launch of `kernel` from the committed PMC pass (profiles/traffic_<kernel>.json:
-    FETCH_SIZE x 2 + WRITE_SIZE per the MI355X guide's gfx950 correction), scaled per document."""
+    FETCH_SIZE x 2 + WRITE_SIZE per the MI355X guide's gfx950 correction).  Only a pass of this
+    exact workload (TRAFFIC_WORKLOAD) at this document count is reported; anything else is None
+    (a pass over another workload says nothing about this launch)."""
     p = os.path.join(ROOT, "profiles", f"traffic_{kernel}.json")
     try:
         t = json.load(open(p))
-        return t["hbm_bytes_per_launch"] / t["docs"] * n_docs
-    except (OSError, KeyError, ZeroDivisionError):
+        if t.get("workload") != TRAFFIC_WORKLOAD.get(kernel) or int(t["docs"]) != n_docs:
+            return None
+        return t["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
         return None
 
 

@@ -183,6 +183,9 @@ int crdt_doc_len(crdt_engine* e, uint64_t n, const uint32_t* doc, uint32_t* len)
 int crdt_doc_status(crdt_engine* e, int32_t* status /* n_docs */);
 /* 64-bit digest of each document's canonical state (DESIGN.md "Digest"; same as the oracle). */
 int crdt_digest(crdt_engine* e, uint64_t* per_doc /* n_docs */);
+/* Canonical spans of each document's published index (YjsSpan::can_append runs; sizes[2] of
+ * crdt_export_sizes for every document at once: the roofline's per-document span counts). */
+int crdt_canon_counts(crdt_engine* e, uint32_t* per_doc /* n_docs */);
 
 /* Export one document (parity / debugging).  sizes[12] = {raw entries, leaves, canonical spans,
  * cwo runs, delete runs, double-delete runs, txns, parents, frontier, agents, next_order, len}.

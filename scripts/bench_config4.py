@@ -29,7 +29,7 @@ ap.add_argument("--cpu-seconds", type=float, default=15.0)
 a = ap.parse_args()
 
 import crdt_amd  # noqa: E402
-from bench import splitmix64, cpu_share, SIMDS  # noqa: E402
+from bench import splitmix64, cpu_share, SIMDS, HBM_PEAK_GBS  # noqa: E402
 
 e = crdt_amd.Engine(a.docs, 32)
 t0 = time.time()
@@ -64,6 +64,7 @@ for _ in range(a.steps):
     rms.append(x.value)
     pms.append(y.value)
 ok = bool((e.status() == 0).all()) and bool((e.digests() == dg0).all())
+canon_total = int(e.canon_counts().astype(np.int64).sum())
 # parity on a sample + the CPU baseline: the oracle on sampled documents, every host core
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from concurrent.futures import ThreadPoolExecutor  # noqa: E402
@@ -95,6 +96,8 @@ def cpu(n):
 
 cdocs, csec = sampled(cpu, threads, a.cpu_seconds, 1 << 20)
 t = min(ts)
+rk = float(np.mean(rms))
+alg = 32 * canon_total + 24 * a.docs * a.ops  # docs x (32 B x canonical spans + 24 B x ops)
 print(json.dumps({
     "metric": "CRDT ops remapped+merged/sec (config 4: on-device random edits)", "value": a.docs * a.ops / t,
     "unit": "ops/s", "n_gpus": 1, "steps": a.steps, "ms_per_step": t * 1e3, "higher_is_better": True,
@@ -102,7 +105,11 @@ print(json.dumps({
     "config": {"workload": f"config4: {a.docs} docs/GPU (1M docs / 8 GPUs) x {a.ops} random ops, replay+publish",
                "docs_per_gpu": a.docs, "ops_per_doc": a.ops, "waves_per_simd": a.docs / SIMDS,
                "hbm_bytes_per_doc": mem / a.docs, "hbm_bytes": mem},
-    "kernels_ms": {"k_replay": float(np.mean(rms)), "k_publish": float(np.mean(pms))},
+    "roofline": {"bound": "hbm", "achieved": alg / (rk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": alg / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "k_replay<32>",
+                 "kernel_ms": rk, "alg_bytes_per_launch": alg, "canonical_spans": canon_total,
+                 "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops)"},
+    "kernels_ms": {"k_replay": rk, "k_publish": float(np.mean(pms))},
     "cpu_baseline": {"value": cdocs * a.ops / csec, "unit": "ops/s", "threads_used": threads,
                      "host_cores": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota,
                      "kind": "port", "sample": f"{cdocs} docs x {a.ops} generated ops on the oracle (reference B-tree "

@@ -1,5 +1,5 @@
 """Profiling driver for k_materialize: stage `docs` copies of the AP remote form, replay, publish,
-share the trace's content stream, then materialise twice; the last k_materialize dispatch of the
+give every document its own copy of the trace's content stream (bench.py's leg), then materialise twice; the last k_materialize dispatch of the
 process is the measured one (same launch as bench.py's materialize leg)."""
 import argparse
 import os
@@ -11,7 +11,8 @@ import crdt_amd  # noqa: E402
 from crdt_amd.traces import content_by_order, load_remote_wire, load_trace  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--docs", type=int, default=4096)
+ap.add_argument("--docs", type=int, default=8192)
+ap.add_argument("--shared", action="store_true", help="one shared content stream (default: a copy per document, as bench.py)")
 ap.add_argument("--trace", default="automerge-paper")
 a = ap.parse_args()
 e = crdt_amd.Engine(a.docs, 32)
@@ -19,7 +20,11 @@ e.stage_remote_replicated(load_remote_wire(a.trace), 0, ["u%05d" % i for i in ra
 st = e.run()
 e.publish_async()
 e.sync()
-e.set_content(list(range(a.docs)), [0] * a.docs, [content_by_order(load_trace(a.trace))])
+c = content_by_order(load_trace(a.trace))
+if a.shared:
+    e.set_content(list(range(a.docs)), [0] * a.docs, [c])
+else:  # bench.py's materialize leg: every document reads its own HBM copy of the content
+    e.set_content_copies(list(range(a.docs)), c)
 for _ in range(2):
     e.materialize_async()
     e.sync()

@@ -11,6 +11,7 @@ docs = int(sys.argv[1])
 out = sys.argv[2] if len(sys.argv) > 2 else "profiles/traffic_k_replay.json"
 kernel = sys.argv[3] if len(sys.argv) > 3 else "k_replay"
 tag = sys.argv[4] if len(sys.argv) > 4 else ""
+workload = sys.argv[5] if len(sys.argv) > 5 else "automerge-paper remote, one clean launch"
 
 
 def last_value(pattern, counter):
@@ -26,7 +27,7 @@ def last_value(pattern, counter):
 fetch_kb, nf = last_value(f"gpurun_out/pmc_fetch{tag}/**/*counter_collection.csv", "FETCH_SIZE")
 write_kb, nw = last_value(f"gpurun_out/pmc_write{tag}/**/*counter_collection.csv", "WRITE_SIZE")
 res = {
-    "kernel": kernel + "<32>", "docs": docs, "workload": "automerge-paper remote, one clean launch",
+    "kernel": kernel + "<32>", "docs": docs, "workload": workload,
     "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
     "hbm_bytes_per_launch": fetch_kb * 1024 * 2 + write_kb * 1024,
     "correction": "FETCH_SIZE x2 (gfx950 wide-read half count), WRITE_SIZE x1",

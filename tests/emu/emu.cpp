@@ -19,6 +19,7 @@ struct EmuDoc {
   AgentTable agents;
   std::vector<Span> leaves;
   std::vector<u32> dir_leaf, dir_vis, sol, leaf_of, parents, frontier;
+  std::vector<u16> agent_of;
   std::vector<CwoRun> cwo;
   std::vector<ARun> arun;
   std::vector<DelRun> dels;
@@ -40,6 +41,7 @@ struct EmuDoc {
     p.dir_vis = dir_vis.data();
     p.slot_of_leaf = sol.data();
     p.leaf_of = leaf_of.data();
+    p.agent_of = agent_of.data();
     p.cwo = cwo.data();
     p.arun = arun.data();
     p.dels = dels.data();
@@ -65,6 +67,7 @@ struct EmuDoc {
     dir_leaf.assign((size_t)c.blk * GROUP, 0);
     dir_vis.assign((size_t)c.blk * GROUP, 0);
     leaf_of.assign(std::max<u32>(c.map, 1), 0xDEADBEEFu);
+    agent_of.assign(std::max<u32>(c.map, 1), 0xBEEFu);
     cwo.assign(c.cwo, CwoRun{});
     arun.assign(c.arun, ARun{});
     dels.assign(c.del, DelRun{});
@@ -88,6 +91,7 @@ struct EmuDoc {
     seg.par_cap = c.par; seg.agent_cap = c.agent; seg.rec_n = (u32)recs.size();
     seg.fr_cap = c.fr; seg.grp_cap = c.blk;
     seg.flags = track ? DOC_TRACK_MAP : 0;
+    if (track && agents.names.size() > 1) seg.flags |= DOC_TRACK_AGENT;  // (as the engine's stage())
     st = DocState{};
     st.n_agents = (u32)agents.names.size();
   }
@@ -113,7 +117,7 @@ struct EmuDoc {
     if (need & 2u) { seg.cwo_cap *= 2; seg.txn_cap *= 2; cwo.resize(seg.cwo_cap); txns.resize(seg.txn_cap); }
     if (need & 4u) { seg.del_cap = seg.del_cap * 2 + 16; dels.resize(seg.del_cap); }
     if (need & 8u) { seg.par_cap = seg.par_cap * 2 + 16; parents.resize(seg.par_cap); }
-    if (need & 16u) { seg.map_cap = seg.map_cap * 2 + 16; leaf_of.resize(seg.map_cap, 0xDEADBEEFu); }
+    if (need & 16u) { seg.map_cap = seg.map_cap * 2 + 16; leaf_of.resize(seg.map_cap, 0xDEADBEEFu); agent_of.resize(seg.map_cap, 0xBEEFu); }
     if (need & 64u) { seg.dd_cap = seg.dd_cap * 2 + 2; dd.resize((size_t)seg.dd_cap * DD_BLK); ddb.resize(seg.dd_cap); }
     if (need & 32u) {  // re-space every agent's run list with doubled capacity
       std::vector<ARun> na;

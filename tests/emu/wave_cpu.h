@@ -4,6 +4,7 @@
 // Never linked into the product library.
 #pragma once
 #include <cstring>
+#include <vector>
 
 #include "crdt_types.h"
 
@@ -12,9 +13,10 @@ namespace crdt {
 template <int L>
 struct WaveCPU {
   Span c[64];
-  u32 gb[ROOT_CAP_MAX], gc[ROOT_CAP_MAX], gv[ROOT_CAP_MAX];
+  std::vector<u32> gb, gc, gv;  // the root, flat (the GPU's two-level root has the same semantics)
+  void root_room(u32 n) { if (gb.size() < n) { gb.resize(n, 0); gc.resize(n, 0); gv.resize(n, 0); } }
 
-  WaveCPU() { std::memset(c, 0, sizeof(c)); std::memset(gb, 0, sizeof(gb)); std::memset(gc, 0, sizeof(gc)); std::memset(gv, 0, sizeof(gv)); }
+  WaveCPU() { std::memset(c, 0, sizeof(c)); }
 
   // context registers (plain array: slot f)
   u32 x[192] = {};
@@ -22,6 +24,7 @@ struct WaveCPU {
   template <class T> static T* gptr(u64 v) { return (T*)v; }
   void xs(u32 f, u32 v) { x[f] = v; }
   void x_pin() {}
+  void bind_root(const Pools&, const DocSeg&) {}
   void x_load_state(const DocState* p, u32 base) { std::memcpy(x + base, p, sizeof(DocState)); }
   void x_store_state(DocState* p, u32 base) const { std::memcpy(p, x + base, sizeof(DocState)); }
 
@@ -50,6 +53,8 @@ struct WaveCPU {
   DocState ld_state(const DocState* p) const { return *p; }
   DocSeg ld_seg(const DocSeg* p) const { return *p; }
   void fill(u32* p, u32 n, u32 v) const { for (u32 k = 0; k < n; k++) p[k] = v; }
+  void fill16(u16* p, u32 n, u32 v) const { for (u32 k = 0; k < n; k++) p[k] = (u16)v; }
+  u32 ld16(const u16* p) const { return *p; }
   void zero_leaf(Span* p, u32 n) const { std::memset(p, 0, sizeof(Span) * n); }
 
   template <class T> static u32 rkey(const T& r) { return ((const u32*)&r)[0]; }
@@ -103,6 +108,20 @@ struct WaveCPU {
   void cset(u32 i, const Span& s) { c[i & 63] = s; }
   template <class F> void cset_lanes(u32 a, u32 b, F f) { for (u32 l = a; l < b && l < 64; l++) c[l] = f(l); }
   u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
+  u32 scan_batch(u32 a, u32 n, u32 X, u32 orr, u32 my_rank, const u16* oag, const AgentRec* agents, u32 tkey,
+                 u32 tlen, u32 tagent, u32& last, u32& last_scan) const {
+    auto agent_of = [&](u32 o) -> u32 { return o - tkey < tlen ? tagent : oag[o]; };
+    u32 f = n;
+    for (u32 j = a; j < n; j++) {
+      u32 rk = agents[agent_of(c[j].order)].rank;
+      bool lt = my_rank > rk;
+      if (c[j].order == orr || c[j].ol != X || (!lt && c[j].orr == orr)) { f = j; break; }
+    }
+    last = f > a ? f - 1u : INVALID;
+    last_scan = 0;
+    if (f > a) last_scan = my_rank > agents[agent_of(c[f - 1].order)].rank ? 0u : 1u;
+    return f;
+  }
   u64 vis_lanes(u32 a, u32 b) const { u64 m = 0; for (u32 i = a; i < b && i < 64; i++) if (c[i].len > 0) m |= 1ull << i; return m; }
   void negate_visible(u32 a, u32 b) { for (u32 i = a; i < b && i < 64; i++) if (c[i].len > 0) c[i].len = -c[i].len; }
   u64 lanes_in(u32 a, u32 b) const { u64 m = 0; for (u32 i = a; i < b && i < 64; i++) m |= 1ull << i; return m; }
@@ -242,7 +261,7 @@ struct WaveCPU {
       bool ok;
       if (remote) {
         const Rec& pr = rb[j + 2];
-        ok = h.w0 == ((REC_RTXN << 28) | 1u) && h.w1 == (agent | (1u << 16)) && h.w2 == ph.w2 + 1u && h.w3 == 1u &&
+        ok = h.w0 == ((REC_RTXN << 28) | (1u << RTXN_DEL_BIT) | 1u) && h.w1 == (agent | (1u << 16)) && h.w2 == ph.w2 + 1u && h.w3 == 1u &&
              o.w0 == ((REC_RDEL << 28) | 1u) && o.w1 == agent && o.w2 == po.w2 + delta &&
              pr.w0 == (REC_RPARENT << 28) && pr.w1 == agent && pr.w2 == h.w2 - 1u;
       } else {
@@ -260,18 +279,23 @@ struct WaveCPU {
 
   // directory root
   void root_init(u32 blk, u32 cnt, u32 vis) {
-    std::memset(gb, 0, sizeof(gb)); std::memset(gc, 0, sizeof(gc)); std::memset(gv, 0, sizeof(gv));
+    gb.assign(64, 0); gc.assign(64, 0); gv.assign(64, 0);
     gb[0] = blk; gc[0] = cnt; gv[0] = vis;
   }
-  void root_load(const GroupRec* g, u32 ng) { for (u32 i = 0; i < ng; i++) { gb[i] = g[i].blk; gc[i] = g[i].cnt; gv[i] = g[i].vis; } }
+  void root_load(const GroupRec* g, u32 ng) {
+    root_room(ng + 1);
+    for (u32 i = 0; i < ng; i++) { gb[i] = g[i].blk; gc[i] = g[i].cnt; gv[i] = g[i].vis; }
+  }
   void root_store(GroupRec* g, u32 ng) const { for (u32 i = 0; i < ng; i++) g[i] = GroupRec{gb[i], gc[i], gv[i], 0}; }
   u32 root_blk(u32 g) const { return gb[g]; }
   u32 root_cnt(u32 g) const { return gc[g]; }
   u32 root_vis(u32 g) const { return gv[g]; }
   u32 root_find_blk(u32 ng, u32 blk) const { for (u32 i = 0; i < ng; i++) if (gb[i] == blk) return i; return INVALID; }
   void root_add_vis(u32 g, u32 d) { gv[g] += d; }
+  void root_add_vis_blk(u32 ng, u32 blk, u32 d) { root_add_vis(root_find_blk(ng, blk), d); }
   void root_set(u32 g, u32 blk, u32 cnt, u32 vis) { gb[g] = blk; gc[g] = cnt; gv[g] = vis; }
   void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
+    root_room(ng + 2);
     for (u32 i = ng; i > g; i--) { gb[i] = gb[i - 1]; gc[i] = gc[i - 1]; gv[i] = gv[i - 1]; }
     root_set(g, blk, cnt, vis);
   }

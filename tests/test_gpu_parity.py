@@ -401,3 +401,46 @@ def test_pos_to_loc_chunks_staged_and_mixed():
         op, od = orc[d].loc_to_pos(ag[m], sq[m])
         assert np.array_equal(gd[m], od), d
         assert np.array_equal(gp[m][od != 2], op[od != 2]), d
+
+
+def test_kevin_reference_size():
+    # The reference's own "kevin" benchmark at its size (benches/yjs.rs:51-62): 5,000,000
+    # single-char local_insert(agent, 0, " ") on one document at the release layout: 5M entries in
+    # 156,250 leaves.  Bit-exact raw layout + leaf boundaries, digest, sampled queries.
+    n = 5_000_000
+    c = np.ones(n, np.uint32)
+    p = np.zeros((n, 3), np.uint32)
+    p[:, 2] = 1
+    e = crdt_amd.Engine(1, 32)
+    ag = e.agent_intern([0], ["seph"])
+    st = e.apply_local_arrays([0], [0, n], np.stack([np.full(n, ag[0]), c], 1).astype(np.uint32), p)
+    assert st[0] == 0, st
+    o = OracleDoc(32, 16)
+    assert o.apply_trace(o.agent("seph"), c, p) == 0
+    assert int(e.lens([0])[0]) == n == len(o)
+    g = e.export(0)
+    assert g["leaf_sizes"].shape[0] == 156_250
+    assert_same(g, o.export())
+    assert int(e.digests()[0]) == o.digest()
+    check_queries_sampled(e, 0, o)
+
+
+def test_kevin_debug_layout_two_level_root():
+    # kevin at the reference size on the debug layout (leaf 4 / node 8): 1.25M leaves in about
+    # 39k directory blocks, past the LDS root's 13,632 groups, so the document replays with the
+    # two-level root (LDS top level over HBM rows of groups).  Bit-exact against the oracle.
+    n = 5_000_000
+    c = np.ones(n, np.uint32)
+    p = np.zeros((n, 3), np.uint32)
+    p[:, 2] = 1
+    e = crdt_amd.Engine(1, 4)
+    ag = e.agent_intern([0], ["seph"])
+    st = e.apply_local_arrays([0], [0, n], np.stack([np.full(n, ag[0]), c], 1).astype(np.uint32), p)
+    assert st[0] == 0, st
+    o = OracleDoc(4, 8)
+    assert o.apply_trace(o.agent("seph"), c, p) == 0
+    g = e.export(0)
+    assert g["leaf_sizes"].shape[0] == 1_250_000
+    assert_same(g, o.export())
+    assert int(e.digests()[0]) == o.digest()
+    check_queries_sampled(e, 0, o)

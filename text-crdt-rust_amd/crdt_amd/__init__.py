@@ -68,6 +68,8 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defin
 # 4 waves/SIMD = 216 ms vs 185 ms), so build() refuses such a library.
 CODEGEN_LIMITS = {
     "k_replay": {"vgpr_count": 64, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
+    # the two-level-root instance (documents past the LDS root) runs at 4 waves per SIMD
+    "k_replay_hr": {"vgpr_count": 128, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
     "k_publish": {"vgpr_count": 64, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
 }
 LLVM_BIN = "/opt/rocm/lib/llvm/bin"
@@ -174,6 +176,8 @@ def lib():
     L.crdt_doc_len.argtypes = [vp, u64, P(u32), P(u32)]
     L.crdt_doc_status.argtypes = [vp, P(i32)]
     L.crdt_digest.argtypes = [vp, P(u64)]
+    if hasattr(L, "crdt_canon_counts"):  # (older libraries, for A/B runs, lack it)
+        L.crdt_canon_counts.argtypes = [vp, P(u32)]
     L.crdt_export_sizes.argtypes = [vp, u32, P(u64)]
     L.crdt_export.argtypes = [vp, u32] + [P(u32)] * 9
     L.crdt_last_timings.argtypes = [vp, P(C.c_double), P(C.c_double)]
@@ -204,7 +208,7 @@ EXPORTED_SYMBOLS = [
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
-    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams",
+    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams",
     # include/crdt_trace.h (host-only trace ingestion)
     "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
@@ -419,6 +423,12 @@ class Engine:
     def digests(self) -> np.ndarray:
         out = np.zeros(self.n_docs, np.uint64)
         _check(self.L.crdt_digest(self.h, _p(out, C.c_uint64)), "digest")
+        return out
+
+    def canon_counts(self) -> np.ndarray:
+        """canonical spans of every document's published index"""
+        out = np.zeros(self.n_docs, np.uint32)
+        _check(self.L.crdt_canon_counts(self.h, _p(out)), "canon_counts")
         return out
 
     def pos_to_loc(self, docs, pos):

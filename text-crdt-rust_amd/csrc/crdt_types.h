@@ -36,6 +36,10 @@ constexpr u32 GROUP = 64;                 // directory slots per block (one wave
 // leaves (every block but the first holds >= 32 slots) = 13.9M entries at the release layout.
 constexpr u32 ROOT_CAP_MIN = 256;
 constexpr u32 ROOT_CAP_MAX = 13632;       // floor(163840 / 12 / 64) * 64
+// Past it the root has two levels (wave_gpu.h HR): LDS top entries of rows that hold 32..64 groups
+// each in HBM, up to ROOT_CAP_MAX - 64 top entries (LDS: 12 B each + two words) -- over 434k
+// groups, 13.9M leaves, 445M entries at the release layout.
+constexpr u32 HROOT_ROW = 192;            // u32 per HBM root row: blk[64], cnt[64], vis[64]
 constexpr u32 FRONTIER_CAP0 = 4;          // initial frontier capacity (grows on demand)
 
 // Status codes (identical to include/crdt_gpu.h and the oracle)
@@ -123,7 +127,7 @@ enum : u32 { REC_LTXN = 1, REC_LOP = 2, REC_RTXN = 3, REC_RINS = 4, REC_RDEL = 5
 struct Rec { u32 w0, w1, w2, w3; };
 // LTXN    w0 = kind<<28 | n_ops         w1 = agent                  w2 = sum(del) w3 = txn_len
 // LOP     w0 = kind<<28                 w1 = pos                    w2 = del   w3 = ins
-// RTXN    w0 = kind<<28 | zero_op<<27 | n_ops (27b)
+// RTXN    w0 = kind<<28 | zero_op<<27 | has_del<<26 | n_ops (26b)
 //                                       w1 = agent | n_parents<<16  w2 = seq   w3 = txn_len
 // RINS    w0 = kind<<28 | len (28b)     w1 = ol_agent | or_agent<<16  w2 = ol_seq  w3 = or_seq
 // RDEL    w0 = kind<<28 | len (28b)     w1 = agent                  w2 = seq
@@ -142,12 +146,14 @@ struct Rec { u32 w0, w1, w2, w3; };
 //         answers pos -> (agent, seq) and (agent, seq) -> (pos, deleted) on the state reached so far
 //         (config 1's per-op check); the answer goes to probe_out[record index]
 CRDT_HD u32 rec_kind(const Rec& r) { return r.w0 >> 28; }
+// RTXN header: has_del (a delete op follows: the double-delete reserve applies, fits()) and n_ops
+constexpr u32 RTXN_DEL_BIT = 26, RTXN_NOPS_MASK = 0x03FFFFFFu;
 constexpr u32 RC_HDR_MASK = 0xF800FFFFu;  // kind | del | author (not len)
 CRDT_HD u32 rc_len(const Rec& r) { return (r.w0 >> 16) & 0x7FFu; }
 // the general records a compact txn stands for (header, op, parent)
 CRDT_HD void expand_rc(const Rec r, Rec& h, Rec& o, Rec& pr) {  // (r by value: h may alias it)
   u32 a = r.w0 & 0xFFFFu, len = rc_len(r);
-  h = Rec{(REC_RTXN << 28) | 1u, a | (1u << 16), r.w1, len};
+  h = Rec{(REC_RTXN << 28) | (((r.w0 >> 27) & 1u) << RTXN_DEL_BIT) | 1u, a | (1u << 16), r.w1, len};
   if ((r.w0 >> 27) & 1u) {
     o = Rec{(REC_RDEL << 28) | len, a, r.w2, 0u};
   } else {
@@ -198,7 +204,10 @@ CRDT_HD Rec gen_op(u32 seed, u32 i, u32 len) {
 // ---------------------------------------------------------------------------------------------
 // DOC_TRACK_MAP: the document keeps its order -> leaf map (the SplitList replacement), which only
 // remote ops read (find_order); documents that only ever apply local ops skip it entirely.
-enum : u32 { DOC_TRACK_MAP = 1u };
+// DOC_TRACK_AGENT: the document also keeps an order -> agent map (u16 per order, same slots as the
+// order -> leaf map): documents with several agents, whose integrate ties read the agent of an
+// entry's first order (doc.rs:207) -- one load instead of a client_with_order search.
+enum : u32 { DOC_TRACK_MAP = 1u, DOC_TRACK_AGENT = 2u };
 
 struct DocSeg {
   u64 leaf_base;   // first leaf (pool index) of this doc; entries at leaf_base*L
@@ -216,6 +225,7 @@ struct DocSeg {
   // words); text (k_materialize) at ord_base (ord_cap code points); ord_cap > every order
   u64 canon_base, pub_base, ord_base;
   u32 canon_cap, ord_cap;
+  u64 hrow_base;   // two-level root documents: first row (192 u32 each) of the HBM root rows
 };
 CRDT_HD u32 pub_words(u32 ord_cap) { return ord_cap / 32u + 1u; }
 
@@ -237,6 +247,7 @@ struct Pools {
   u32* dir_vis;
   u32* slot_of_leaf;   // [leaf_base + leaf] = blk<<6 | i
   u32* leaf_of;        // [map_base + order]
+  u16* agent_of;       // [map_base + order] (DOC_TRACK_AGENT documents)
   CwoRun* cwo;
   ARun* arun;
   DelRun* dels;
@@ -248,6 +259,8 @@ struct Pools {
   u32* frontier;       // [fr_base .. + fr_cap]
   AgentRec* agents;
   GroupRec* groups;    // [grp_base .. + grp_cap]
+  u32* hrows;          // [hrow_base * 192 ..]: two-level root rows (kernels launched with an HBM root)
+  u32* gsob;           // [blk_base + block]: row << 6 | slot of each block's group (same)
   const Rec* recs;
   const DocSeg* seg;
   DocState* st;

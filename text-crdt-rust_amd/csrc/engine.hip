@@ -49,6 +49,9 @@ struct PoolSet {
   u32* dir_leaf = nullptr;
   u32* dir_vis = nullptr;
   u32* leaf_of = nullptr;
+  u16* agent_of = nullptr;  // (allocated for every map slot when some document keeps it)
+  u32* hrows = nullptr;     // two-level root rows (documents past the LDS root)
+  u32* gsob = nullptr;      // their blocks' row slots (every block slot when some document needs it)
   CwoRun* cwo = nullptr;
   ARun* arun = nullptr;
   DelRun* dels = nullptr;
@@ -61,7 +64,7 @@ struct PoolSet {
   AgentRec* agents = nullptr;
   u64 bytes = 0;
   void free_all() {
-    dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(cwo); dfree(arun);
+    dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(agent_of); dfree(hrows); dfree(gsob); dfree(cwo); dfree(arun);
     dfree(dels); dfree(dd); dfree(ddb); dfree(txns); dfree(parents); dfree(frontier); dfree(groups); dfree(agents);
     bytes = 0;
   }
@@ -73,6 +76,7 @@ struct DocHost {
   StreamNeeds staged;       // needs of the stream staged now (a reset replays it: cum = staged)
   Caps caps{};              // current capacities (grow; crdt_fit shrinks them to the replay's use)
   bool tracked = false;     // keeps the order -> leaf map (once a remote stream was staged)
+  bool agent_map = false;   // keeps the order -> agent map (tracked, and more than one agent)
   std::vector<u32> agent_cap;
 };
 
@@ -82,15 +86,17 @@ inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
   if (c.txns_per_agent.size() < n.txns_per_agent.size()) c.txns_per_agent.resize(n.txns_per_agent.size(), 0);
   for (size_t a = 0; a < n.txns_per_agent.size(); a++) c.txns_per_agent[a] += n.txns_per_agent[a];
   c.txn_max(n.max_ops, n.max_del, n.max_len, n.max_parents);
+  c.max_rdel_len = std::max(c.max_rdel_len, n.max_rdel_len);
   c.probes += n.probes;
   c.local_del_ops += n.local_del_ops;
 }
 
 // Launch shape of a wave-per-document kernel whose waves hold an LDS root of `rcap` groups:
 // up to 4 waves per workgroup within the 160 KiB a workgroup may declare.
+// (hr: the two-level root: rcap top entries + two words per wave)
 struct LaunchShape { u32 wpb, rcap; size_t lds; };
-inline LaunchShape launch_shape(u32 rcap) {
-  u32 per_wave = 12u * rcap;
+inline LaunchShape launch_shape(u32 rcap, bool hr = false) {
+  u32 per_wave = 12u * rcap + (hr ? 8u : 0u);
   u32 wpb = std::max<u32>(1u, std::min<u32>(WAVES_PER_BLOCK, 163840u / per_wave));
   return LaunchShape{wpb, rcap, (size_t)wpb * per_wave};
 }
@@ -98,7 +104,17 @@ inline LaunchShape launch_shape(u32 rcap) {
 constexpr u32 ROOT_CLASSES[4] = {ROOT_CAP_MIN, 1024, 4096, ROOT_CAP_MAX};
 inline u32 root_class(u32 grp_cap) {
   for (u32 c : ROOT_CLASSES) if (grp_cap <= c) return c;
-  return 0;  // cannot be held (the host never plans this)
+  return 0;  // past the LDS root: the two-level root (hroot_top)
+}
+// Documents whose root groups exceed the LDS root replay with the two-level root (wave_gpu.h HR):
+// rows of 32..64 groups in HBM (<= grp_cap/32 + 2 of them) under an LDS top level of that many
+// entries.  CRDT_FORCE_HBM_ROOT=1 puts every document there (tests of the two-level root).
+// (read at every layout: tests switch it per engine)
+thread_local bool g_force_hroot = false;
+inline bool uses_hroot(u32 grp_cap) { return g_force_hroot || root_class(grp_cap) == 0; }
+inline u32 hroot_rows(u32 grp_cap) { return grp_cap / 32u + 2u; }
+inline u32 hroot_top(u32 grp_cap) {  // LDS top entries per wave (a multiple of 64)
+  return (hroot_rows(grp_cap) + 63u) & ~63u;
 }
 
 }  // namespace
@@ -121,7 +137,7 @@ struct crdt_engine {
   u32* n_agents_d = nullptr;
   std::vector<u32> n_agents_pushed;  // host copy of what n_agents_d holds
   // replay launches: one per LDS root class present; `doc_list` holds the classes' documents
-  struct RootClass { u32 rcap; u64 off, n; };
+  struct RootClass { u32 rcap; u64 off, n; bool hr; };
   std::vector<RootClass> classes;
   u32* doc_list = nullptr;
   PoolSet pools;
@@ -171,6 +187,9 @@ struct crdt_engine {
     p.dir_vis = ps.dir_vis;
     p.slot_of_leaf = ps.sol;
     p.leaf_of = ps.leaf_of;
+    p.agent_of = ps.agent_of;
+    p.hrows = ps.hrows;
+    p.gsob = ps.gsob;
     p.cwo = ps.cwo;
     p.arun = ps.arun;
     p.dels = ps.dels;
@@ -264,11 +283,14 @@ struct crdt_engine {
   // existing state into it (k_relayout), else just install it.
   int layout(bool move) {
     int r = 0;
+    g_force_hroot = getenv("CRDT_FORCE_HBM_ROOT") != nullptr && getenv("CRDT_FORCE_HBM_ROOT")[0] == '1';
     PoolSet np;
     u64 nl = 0, nb = 0, nm = 0, nc = 0, na = 0, ndl = 0, ndd = 0, nt = 0, npar = 0, nag = 0, nfr = 0;
     std::vector<DocSeg> nseg(n_docs);
     std::vector<AgentRec> agent_tab;
     std::vector<u32> n_agents(n_docs);
+    bool any_agent_map = false, any_hroot = false;
+    u64 nhr = 0;
     for (u64 d = 0; d < n_docs; d++) {
       DocHost& h = docs[d];
       const Caps& c = h.caps;
@@ -285,6 +307,8 @@ struct crdt_engine {
       s.canon_base = seg_h[d].canon_base; s.canon_cap = seg_h[d].canon_cap;  // (size_pub's)
       s.pub_base = seg_h[d].pub_base; s.ord_base = seg_h[d].ord_base; s.ord_cap = seg_h[d].ord_cap;
       s.grp_base = s.blk_base; s.grp_cap = c.blk;  // one root group per directory block
+      s.hrow_base = nhr;
+      if (uses_hroot(c.blk)) { nhr += hroot_rows(c.blk); any_hroot = true; }
       s.agent_base = nag;
       u32 ag = (u32)h.agents.names.size();
       s.agent_cap = ag;
@@ -303,7 +327,8 @@ struct crdt_engine {
       s.arun_cap = rb;
       na += rb;
       nag += ag;
-      s.flags = h.tracked ? DOC_TRACK_MAP : 0u;
+      s.flags = (h.tracked ? DOC_TRACK_MAP : 0u) | (h.agent_map ? DOC_TRACK_AGENT : 0u);
+      any_agent_map |= h.agent_map;
       s.rec_base = seg_h[d].rec_base;
       s.rec_n = seg_h[d].rec_n;
       nseg[d] = s;
@@ -313,6 +338,9 @@ struct crdt_engine {
     HIPCHK(dalloc(np.dir_leaf, nb * GROUP));
     HIPCHK(dalloc(np.dir_vis, nb * GROUP));
     HIPCHK(dalloc(np.leaf_of, nm));
+    HIPCHK(dalloc(np.agent_of, any_agent_map ? nm : 1));
+    HIPCHK(dalloc(np.hrows, any_hroot ? nhr * HROOT_ROW : 1));
+    HIPCHK(dalloc(np.gsob, any_hroot ? nb : 1));
     HIPCHK(dalloc(np.cwo, nc));
     HIPCHK(dalloc(np.arun, na));
     HIPCHK(dalloc(np.dels, ndl));
@@ -323,8 +351,14 @@ struct crdt_engine {
     HIPCHK(dalloc(np.frontier, nfr));
     HIPCHK(dalloc(np.groups, nb));
     HIPCHK(dalloc(np.agents, nag));
-    np.bytes = nl * L * 16 + nl * 4 + nb * GROUP * 8 + nm * 4 + nc * 16 + na * 16 + ndl * 12 +
+    np.bytes = nl * L * 16 + nl * 4 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) +
+               (any_hroot ? nhr * HROOT_ROW * 4 + nb * 4 : 0) + nc * 16 + na * 16 + ndl * 12 +
                ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * 16 + nfr * 4 + nb * 16;
+    if (getenv("CRDT_DEBUG_MEM"))
+      fprintf(stderr, "layout: leaves %llu blocks %llu map %llu cwo %llu arun %llu del %llu ddblk %llu txn %llu par %llu agents %llu fr %llu -> %.1f MB\n",
+              (unsigned long long)nl, (unsigned long long)nb, (unsigned long long)nm, (unsigned long long)nc,
+              (unsigned long long)na, (unsigned long long)ndl, (unsigned long long)ndd, (unsigned long long)nt,
+              (unsigned long long)npar, (unsigned long long)nag, (unsigned long long)nfr, np.bytes / 1e6);
     if (!agent_tab.empty())
       HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(n_agents_d, n_agents.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
@@ -417,26 +451,39 @@ struct crdt_engine {
   // Replay launch classes (LDS root sizes) from the documents' root capacities; the documents
   // of every class go to the device list when more than one class is present.
   int plan_classes() {
-    std::vector<std::vector<u32>> by(4);
+    // classes 0-3: the LDS root sizes; class 4: the two-level root (top size: the largest needed)
+    std::vector<std::vector<u32>> by(5);
+    u32 hr_top = 64;
     for (u64 d = 0; d < n_docs; d++) {
-      u32 c = root_class(seg_h[d].grp_cap);
+      u32 gc = seg_h[d].grp_cap;
+      if (uses_hroot(gc)) {
+        by[4].push_back((u32)d);
+        hr_top = std::max(hr_top, hroot_top(gc));
+        continue;
+      }
+      u32 c = root_class(gc);
       u32 k = 0;
       while (ROOT_CLASSES[k] != c) k++;
       by[k].push_back((u32)d);
     }
+    if (hr_top > ROOT_CAP_MAX) {
+      g_last_error = "a document's root exceeds the two-level root's top level";
+      return CRDT_E_NOMEM;
+    }
+    auto rc = [&](u32 k) { return k < 4 ? ROOT_CLASSES[k] : hr_top; };
     classes.clear();
     dfree(doc_list);
     u32 present = 0;
     for (auto& v : by) present += !v.empty();
     if (present <= 1) {
-      for (u32 k = 0; k < 4; k++)
-        if (!by[k].empty()) classes.push_back(RootClass{ROOT_CLASSES[k], INVALID, by[k].size()});
+      for (u32 k = 0; k < 5; k++)
+        if (!by[k].empty()) classes.push_back(RootClass{rc(k), INVALID, by[k].size(), k == 4});
       return 0;
     }
     std::vector<u32> all;
-    for (u32 k = 0; k < 4; k++) {
+    for (u32 k = 0; k < 5; k++) {
       if (by[k].empty()) continue;
-      classes.push_back(RootClass{ROOT_CLASSES[k], all.size(), by[k].size()});
+      classes.push_back(RootClass{rc(k), all.size(), by[k].size(), k == 4});
       all.insert(all.end(), by[k].begin(), by[k].end());
     }
     HIPCHK(dalloc(doc_list, all.size()));
@@ -519,6 +566,21 @@ struct crdt_engine {
         pulled = true;
       }
       if (st_h[doc_ids[i]].next_order) rebuild.push_back((u32)doc_ids[i]);
+    }
+    // tracked documents with several agents keep the order -> agent map too (integrate's name
+    // tie-breaks); one that already holds state gets it rebuilt from client_with_order
+    std::vector<u32> rebuild_ag;
+    for (size_t i = 0; i < doc_ids.size(); i++) {
+      DocHost& h = docs[doc_ids[i]];
+      if (h.agent_map || !h.tracked || h.agents.names.size() < 2) continue;
+      h.agent_map = true;
+      grow = true;
+      if (!pulled) {
+        r = pull_states();
+        if (r) return r;
+        pulled = true;
+      }
+      if (st_h[doc_ids[i]].next_order) rebuild_ag.push_back((u32)doc_ids[i]);
     }
     // cumulative needs -> capacities
     for (size_t i = 0; i < doc_ids.size(); i++) {
@@ -632,6 +694,15 @@ struct crdt_engine {
         HIPCHK(hipStreamSynchronize(stream));
         dfree(dl);
       }
+      if (!rebuild_ag.empty()) {
+        u32* dl = nullptr;
+        HIPCHK(dalloc(dl, rebuild_ag.size()));
+        HIPCHK(hipMemcpyAsync(dl, rebuild_ag.data(), rebuild_ag.size() * 4, hipMemcpyHostToDevice, stream));
+        hipLaunchKernelGGL(k_build_agent_map, dim3((u32)rebuild_ag.size()), dim3(256), 0, stream, pools_view(pools), (const u32*)dl, (u32)rebuild_ag.size());
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(stream));
+        dfree(dl);
+      }
     } else {
       HIPCHK(hipMemcpyAsync(segs, seg_h.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
       r = push_agent_counts();
@@ -650,12 +721,17 @@ struct crdt_engine {
   int launch_replay() {
     if (!n_docs) return 0;
     Pools pv = pools_view(pools);
-    for (const RootClass& c : classes) {  // one launch per LDS root class (usually one)
-      LaunchShape sh = launch_shape(c.rcap);
+    for (const RootClass& c : classes) {  // one launch per root class (usually one)
+      LaunchShape sh = launch_shape(c.rcap, c.hr);
       u32 blocks = (u32)((c.n + sh.wpb - 1) / sh.wpb);
       const u32* list = c.off == INVALID ? nullptr : doc_list + c.off;
-      if (L == 32) hipLaunchKernelGGL(k_replay<32>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
-      else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+      if (c.hr) {
+        if (L == 32) hipLaunchKernelGGL(k_replay_hr<32>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+        else hipLaunchKernelGGL(k_replay_hr<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+      } else {
+        if (L == 32) hipLaunchKernelGGL(k_replay<32>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+        else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+      }
       HIPCHK(hipGetLastError());
     }
     if (!pub_fitted) pub_sized = false;  // the state grows: size the index again before publishing
@@ -746,6 +822,12 @@ struct crdt_engine {
       c.ord = s.next_order + 1;
       c.canon = std::max<u32>(cn[d], 1);
       c.fr = std::max<u32>(s.n_fr + 1, FRONTIER_CAP0);
+      // double-delete blocks: fits()' reserve before the stream's last remote delete txn (the
+      // entry count only grows, so the final count bounds every earlier reserve)
+      if (c.dd) {
+        u64 ov = std::min<u64>(s.n_dd, m.max_rdel_len);
+        c.dd = std::max<u32>(4u, (u32)std::min<u64>(((u64)s.n_dd + 3 * ov + 2ull * m.max_rdel_len + 2) / 32 + 3, 0x7FFFFFFFull));
+      }
     }
     r = layout(true);
     if (r) return r;
@@ -944,6 +1026,8 @@ int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
   // the replay's LDS root may take a workgroup's whole 160 KiB (one wave per workgroup)
   (void)hipFuncSetAttribute((const void*)k_replay<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay_hr<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay_hr<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<32>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);
   (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<4>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);
   (void)hipFuncSetAttribute((const void*)k_loc_to_pos_blk<32>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_W * 8u);
@@ -1431,6 +1515,15 @@ int crdt_digest(crdt_engine* e, uint64_t* per_doc) {
   int r = e->ensure_published();
   if (r) return r;
   HIPCHK(hipMemcpyAsync(per_doc, e->digest, e->n_docs * 8, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return 0;
+}
+
+int crdt_canon_counts(crdt_engine* e, uint32_t* per_doc) {
+  if (!valid(e) || !per_doc) return CRDT_E_ARG;
+  int r = e->ensure_published();
+  if (r) return r;
+  HIPCHK(hipMemcpyAsync(per_doc, e->canon_n, e->n_docs * 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   return 0;
 }

@@ -100,6 +100,7 @@ struct StreamNeeds {
   u32 max_ops = 0, max_del = 0, max_len = 0, max_parents = 0;
   u64 probes = 0;  // PROBE records (their documents keep the order -> leaf map)
   u64 local_del_ops = 0;  // LocalOps that delete
+  u32 max_rdel_len = 0;   // longest remote txn with a delete op (the double-delete reserve, fits())
   std::vector<u32> txns_per_agent;
   void txn_max(u32 ops, u64 del, u64 len, u32 parents) {
     max_ops = std::max(max_ops, ops);
@@ -162,6 +163,9 @@ inline void encode_remote(std::vector<Rec>& out, StreamNeeds& nd, AgentTable& at
     }
     u32 tl32 = tl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (u32)tl;
     nd.txn_max(t.n_ops, t.n_ops, tl, t.n_parents);
+    u32 has_del = 0;
+    for (u32 k = 0; k < t.n_ops; k++)
+      if (t.ops[6 * k] != 0) { has_del = 1; nd.max_rdel_len = std::max<u32>(nd.max_rdel_len, tl32); break; }
     // the common shape -- one op on the author's own items (or ROOT), the author's previous txn
     // as the only parent -- is one compact record (crdt_types.h RC)
     if (t.n_ops == 1 && t.n_parents == 1 && author < 0xFFFEu && t.seq >= 1 && res(t.parents[0]) == author &&
@@ -190,7 +194,8 @@ inline void encode_remote(std::vector<Rec>& out, StreamNeeds& nd, AgentTable& at
         continue;
       }
     }
-    out.push_back(Rec{(REC_RTXN << 28) | ((zero ? 1u : 0u) << 27) | (t.n_ops & 0x07FFFFFFu),
+    if (t.n_ops > RTXN_NOPS_MASK) zero = true;  // (no stream holds such a txn: rejected as malformed)
+    out.push_back(Rec{(REC_RTXN << 28) | ((zero ? 1u : 0u) << 27) | (has_del << RTXN_DEL_BIT) | (t.n_ops & RTXN_NOPS_MASK),
                       (author & 0xFFFFu) | ((t.n_parents & 0xFFFFu) << 16), t.seq, tl32});
     for (u32 k = 0; k < t.n_ops; k++) {
       const u32* o = t.ops + 6 * k;
@@ -239,8 +244,9 @@ inline void encode_gen(std::vector<Rec>& out, StreamNeeds& nd, u32 agent, u32 n_
 
 // Capacities for a fresh document that will apply `nd` (heuristic leaf capacity; everything
 // else is an upper bound).  Growth for leaves/blocks is handled by the caller on ST_CAPACITY.
-// Leaves are bounded only by the LDS root: blk_cap = leaf_cap/32 + 2 <= ROOT_CAP_MAX groups.
-constexpr u32 MAX_LEAVES = 32 * (ROOT_CAP_MAX - 2);
+// Leaves are bounded only by the two-level root's LDS top level: blk_cap = leaf_cap/32 + 2 groups
+// in rows of >= 32, under <= ROOT_CAP_MAX top entries (engine.hip hroot_top).
+constexpr u32 MAX_LEAVES = 32u * 32u * (ROOT_CAP_MAX - 64u);
 
 struct Caps {
   u32 leaf, blk, map, cwo, arun, del, dd, txn, par, agent, fr;
@@ -277,7 +283,7 @@ inline Caps plan_caps(const StreamNeeds& nd, u32 n_agents, bool track, u32 leaf_
   // double-delete blocks: grown on demand (rare but for config 5).  fits() reserves
   // (4 * entries + 2 * txn_len + 2) / 32 + 2 blocks before a remote delete txn, so the first
   // capacity covers the stream's longest txn on an empty table: no relaunch just for its reserve.
-  c.dd = nd.remote_del_ops ? std::max<u32>(4u, (u32)std::min<u64>((2ull * nd.max_len + 2) / 32 + 3, 0x7FFFFFFFull)) : 0u;
+  c.dd = nd.remote_del_ops ? std::max<u32>(4u, (u32)std::min<u64>((2ull * nd.max_rdel_len + 2) / 32 + 3, 0x7FFFFFFFull)) : 0u;
   c.par = (u32)std::min<u64>(nd.remote_parents + nd.n_txn + 64 + 1, 1024 + (nd.remote_parents + nd.n_txn) / 64);
   c.agent = n_agents;
   return c;

@@ -52,13 +52,13 @@ __device__ __forceinline__ u32 span_of_order(const PubOut& O, const DocSeg& seg,
 // Dynamic LDS of the wave-per-document kernels: each wave's directory root, 3 x rcap u32
 // (launch shape: engine.hip launch_shape).
 extern __shared__ u32 s_dyn[];
-template <int L>
-__device__ __forceinline__ WaveGPU<L> wave_with_root(u32 rcap) {
-  WaveGPU<L> w;
+template <int L, bool HR = false>
+__device__ __forceinline__ WaveGPU<L, HR> wave_with_root(u32 rcap) {
+  WaveGPU<L, HR> w;
   // the LDS address space survives into the member: root accesses are ds_* (lgkmcnt only);
   // a generic pointer would make them flat ops, whose waits also drain every pending store
   w.rcap = rcap;
-  w.rt = (typename WaveGPU<L>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * 3u * rcap);
+  w.rt = (typename WaveGPU<L, HR>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * (3u * rcap + (HR ? 2u : 0u)));
   return w;
 }
 // Document of the calling wave: wave k of the launch takes list[k] (or k without a list).
@@ -86,12 +86,12 @@ __global__ __launch_bounds__(256) void k_init(Pools P, u32 n, u32 wpb, u32 rcap)
 // documents in 185 ms where the compiler's own choice (84 VGPRs: 5 waves/SIMD) takes 199 ms and
 // 97 VGPRs (4 waves/SIMD) took 216 ms (scripts/gpu_ab.sh).  What the budget costs is a few spills
 // in cold paths.
-template <int L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
+template <int L, bool HR>
+__device__ __forceinline__ void replay_doc(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
   u32 d;
   if (!wave_doc(wpb, list, n, d)) return;
-  Replayer<WaveGPU<L>, L> r(P, d, wave_with_root<L>(rcap));
-  WaveGPU<L>& w = r.w;
+  Replayer<WaveGPU<L, HR>, L> r(P, d, wave_with_root<L, HR>(rcap));
+  WaveGPU<L, HR>& w = r.w;
   if (r.status() == ST_NEED_CAPACITY) r.p(S_STATUS, (u32)ST_OK);  // resume after growth
   if (r.status() != ST_OK || r.g(S_REC_POS) >= r.rec_n()) {
     w.st((u32*)&P.st[d].status, (u32)r.status());
@@ -100,6 +100,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   r.begin();
   r.run();
   r.finish();
+}
+template <int L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
+  replay_doc<L, false>(P, n, wpb, rcap, list);
+}
+// Documents past the LDS root replay with the two-level root (wave_gpu.h HR).  They are few and
+// long, so this instance is held to 4 waves per SIMD (<= 128 VGPRs: no scratch for its extra
+// root state) instead of the batch kernel's 8.
+template <int L>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_replay_hr(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
+  replay_doc<L, true>(P, n, wpb, rcap, list);
 }
 
 // Reset the per-call record cursor of every document (new stream staged).
@@ -132,6 +143,7 @@ __global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const Do
   bcopy(dst.dir_leaf + w.blk_base * GROUP, src.dir_leaf + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
   bcopy(dst.dir_vis + w.blk_base * GROUP, src.dir_vis + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
   if (w.flags & o.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);
+  if (w.flags & o.flags & DOC_TRACK_AGENT) bcopy(dst.agent_of + w.map_base, src.agent_of + o.map_base, s.next_order);
   bcopy(dst.cwo + w.cwo_base, src.cwo + o.cwo_base, s.n_cwo);
   bcopy(dst.dels + w.del_base, src.dels + o.del_base, s.n_del);
   bcopy(dst.dd + w.dd_base * DD_BLK, src.dd + o.dd_base * DD_BLK, (u64)s.n_ddb * DD_BLK);
@@ -174,6 +186,21 @@ __global__ __launch_bounds__(256) void k_build_map(Pools P, const u32* docs, u32
         for (u32 t = threadIdx.x; t < slen(sp); t += blockDim.x) lof[sp.order + t] = leaf;
       }
     }
+  }
+}
+
+// Order -> agent map of documents that start keeping it (a second agent appears in a tracked
+// document that already holds state): every client_with_order run's orders -> its agent.
+__global__ __launch_bounds__(256) void k_build_agent_map(Pools P, const u32* docs, u32 n) {
+  if (blockIdx.x >= n) return;
+  u32 d = docs[blockIdx.x];
+  DocState s = P.st[d];
+  DocSeg sg = P.seg[d];
+  u16* oag = P.agent_of + sg.map_base;
+  const CwoRun* cw = P.cwo + sg.cwo_base;
+  for (u32 k = 0; k < s.n_cwo; k++) {
+    CwoRun r = cw[k];  // (the last run's length is current: the replay's tails were flushed)
+    for (u32 t = threadIdx.x; t < r.len; t += blockDim.x) oag[r.key + t] = (u16)r.agent;
   }
 }
 

@@ -56,6 +56,8 @@ enum : u32 {
   P_PROBE = P_DDB + 2,    // (2 slots) probe answers
   K_LEAF = P_PROBE + 2, K_MAP, K_CWO, K_TXN, K_DEL, K_DD, K_PAR, K_RECN,
   K_FR,                   // frontier capacity
+  P_OAG,                  // (2 slots) order -> agent map
+  K_AGMAP = P_OAG + 2,    // 1: the document keeps the order -> agent map (DOC_TRACK_AGENT)
   // x1: DocState, field for field (struct order), then the per-call flags
   S_BASE = 64,
   S_STATUS = 64, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
@@ -82,7 +84,7 @@ enum : u32 {
   T_AGL_KEY, T_AGL_ORDER, T_AGL_LEN,
   N_SLOTS
 };
-static_assert(K_FR < 64, "read-only slots live in the first context register");
+static_assert(K_AGMAP < 64, "read-only slots live in the first context register");
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
 static_assert(T_RB_BASE < 128, "DocState and the flags live in the second context register");
 static_assert(N_SLOTS <= 192, "three context registers");
@@ -124,6 +126,7 @@ struct Replayer {
   CRDT_HD u32* dv() const { return ptr<u32>(P_DV); }
   CRDT_HD u32* sol() const { return ptr<u32>(P_SOL); }
   CRDT_HD u32* lof() const { return ptr<u32>(P_LOF); }
+  CRDT_HD u16* oag() const { return ptr<u16>(P_OAG); }
   CRDT_HD CwoRun* cwo() const { return ptr<CwoRun>(P_CWO); }
   CRDT_HD ARun* arun() const { return ptr<ARun>(P_ARUN); }
   CRDT_HD DelRun* dels() const { return ptr<DelRun>(P_DELS); }
@@ -144,11 +147,13 @@ struct Replayer {
     prof_mode = d & 3u;
 #endif
     DocSeg sg = w.ld_seg(P.seg + d);
+    w.bind_root(P, sg);  // (the two-level root's HBM rows, for documents past the LDS root)
     pset(P_LV, P.leaves + sg.leaf_base * (u64)L);
     pset(P_DL, P.dir_leaf + sg.blk_base * (u64)GROUP);
     pset(P_DV, P.dir_vis + sg.blk_base * (u64)GROUP);
     pset(P_SOL, P.slot_of_leaf + sg.leaf_base);
     pset(P_LOF, P.leaf_of + sg.map_base);
+    pset(P_OAG, P.agent_of + sg.map_base);
     pset(P_CWO, P.cwo + sg.cwo_base);
     pset(P_ARUN, P.arun + sg.arun_base);
     pset(P_DELS, P.dels + sg.del_base);
@@ -171,6 +176,7 @@ struct Replayer {
     p(K_PAR, sg.par_cap);
     p(K_RECN, sg.rec_n);
     p(K_FR, sg.fr_cap);
+    p(K_AGMAP, (sg.flags & DOC_TRACK_AGENT) ? 1u : 0u);
     w.x_load_state(P.st + d, S_BASE);
     p(C_LEAF, INVALID);
     p(C_N, 0);
@@ -244,6 +250,7 @@ struct Replayer {
   }
   // write-back tails -> HBM (the tables' last entries; frontier[0])
   CRDT_HD void flush_tails() {
+    agent_fill_tail();
     u32 n = g(S_N_CWO);
     if (n) w.st(&w.at(cwo(), n - 1)->len, g(T_CWO_LEN));
     n = g(S_N_DEL);
@@ -323,7 +330,7 @@ struct Replayer {
     if (v == old) return;
     u32 blk = g(C_BLK);
     w.st(dvis(blk) + g(C_I), v);
-    w.root_add_vis(w.root_find_blk(g(S_NG), blk), v - old);
+    w.root_add_vis_blk(g(S_NG), blk, v - old);
     inc(S_LEN, v - old);
     p(C_VIS, v);
   }
@@ -721,10 +728,23 @@ struct Replayer {
   CRDT_HD bool order_to_agent(u32 order, u32& agent) const {  // client_with_order.get()
     u32 n = g(S_N_CWO), key = g(T_CWO_KEY);
     if (order - key < g(T_CWO_LEN)) { agent = g(T_CWO_AGENT); return true; }
+    if (g(K_AGMAP)) {  // the order -> agent map (every assigned order has its author there)
+      if (order >= g(S_NEXT_ORDER)) return false;
+      agent = w.ld16(w.at(oag(), order));
+      return true;
+    }
     i32 k = w.search_cwo(cwo(), n, order);
     if (k < 0) return false;
     agent = w.ld_cwo(w.at(cwo(), (u32)k)).agent;
     return true;
+  }
+  // The order -> agent map, if kept, is written when a client_with_order run is retired (a new
+  // run starts) and at the end of a launch: order_to_agent answers the current tail run from the
+  // context lanes, so the fast paths, which only extend the tail, write nothing.
+  CRDT_HD void agent_fill_tail() {
+    if (g(K_AGMAP)) {
+      if (g(S_N_CWO)) w.fill16(w.at(oag(), g(T_CWO_KEY)), g(T_CWO_LEN), g(T_CWO_AGENT));
+    }
   }
   // doc.rs:155-165 assign_order_to_client
   CRDT_HD void assign_order_to_client(u32 agent, u32 seq, u32 order, u32 len) {
@@ -734,6 +754,7 @@ struct Replayer {
       p(T_CWO_LEN, cl + len);
     } else {
       if (n) w.st(&w.at(cwo(), n - 1)->len, cl);  // retire the old tail
+      agent_fill_tail();
       p(T_CWO_KEY, order); p(T_CWO_AGENT, agent); p(T_CWO_SEQ, seq); p(T_CWO_LEN, len);
       w.st_cwo(w.at(cwo(), n), CwoRun{order, agent, seq, len});
       p(S_N_CWO, n + 1);
@@ -972,10 +993,14 @@ struct Replayer {
     if (g(K_MAP) - g(S_NEXT_ORDER) < txn_len) need |= 16u;
     if (remote && g(K_FR) <= g(S_N_FR)) need |= 128u;  // a remote txn leaves <= nfr + 1 heads
     // double deletes (remote only): one txn adds at most 3 entries per existing entry it overlaps
+    // (entries are disjoint runs of >= 1 item, so it overlaps <= min(entries, txn_len) of them)
     // plus 2 per increment_delete_range call (<= one per deleted item); every block but the
     // first holds >= 32 entries, so E entries need <= E/32 + 1 blocks
     u32 ndd = g(S_N_DD);
-    if (remote && n_dels && (4ull * ndd + 2ull * txn_len + 2ull) / 32ull + 2ull > (u64)g(K_DD)) need |= 64u;
+    if (remote && n_dels) {
+      u64 ov = ndd < txn_len ? ndd : txn_len;
+      if ((ndd + 3ull * ov + 2ull * txn_len + 2ull) / 32ull + 2ull > (u64)g(K_DD)) need |= 64u;
+    }
     use_agent(agent);
     if (g(T_AG_CAP) == g(T_AG_CNT)) need |= 32u;
     p(S_CAP_NEED, need);
@@ -1005,7 +1030,7 @@ struct Replayer {
       if (!fits(false, agent, nops, h.w2, txn_len, 0)) return ST_NEED_CAPACITY;
       seq = agent_next_seq(agent);
     } else {
-      nops = h.w0 & 0x07FFFFFFu;
+      nops = h.w0 & RTXN_NOPS_MASK;
       agent = h.w1 & 0xFFFFu;
       np = h.w1 >> 16;
       seq = h.w2;
@@ -1014,7 +1039,8 @@ struct Replayer {
       if (agent_next_seq(agent) != seq) return ST_SEQ;
       if ((h.w0 >> 27) & 1u) return ST_BAD_INPUT;
       if (txn_len == 0) return ST_EMPTY_TXN;
-      if (!fits(true, agent, nops, nops, txn_len, np)) return ST_NEED_CAPACITY;
+      // (delete-log and double-delete room only for a txn with a delete op: RTXN has_del)
+      if (!fits(true, agent, nops, ((h.w0 >> RTXN_DEL_BIT) & 1u) ? nops : 0u, txn_len, np)) return ST_NEED_CAPACITY;
     }
     u32 first = g(S_NEXT_ORDER);
     u32 next = first;
@@ -1108,7 +1134,36 @@ struct Replayer {
         // integrate (doc.rs:167-234): scan entries from the insertion point
         Cursor left = c, scan_start = c;
         bool scanning = false;
+        u32 first_step = 1;
         while (true) {
+          // From the second step on the cursor sits at the start of an entry of the cached leaf
+          // (next_entry), so the entry's item is its first order and its origin_left is the
+          // entry's ol: the leaf's entries from the cursor on are evaluated lane-parallel
+          // (W::scan_batch: one gather of their first orders' agents and ranks).  An entry whose
+          // origin_left is integrate's own (cmp == 0 by identity: cursor_after of one item) and
+          // that does not break changes only (scanning, scan_start), and the last such entry
+          // before the first event decides them; the first event -- origin_right reached, a
+          // tie that breaks, or an origin_left elsewhere (a real cursor compare) -- is then
+          // evaluated by the sequential step below.  Documents without the order -> agent map
+          // take every step sequentially.
+          if (!first_step) {
+            if (g(K_AGMAP)) {
+              u32 nn = g(C_N), last, last_scan;
+              u32 f = w.scan_batch(c.idx, nn, item.ol, item.orr, w.ld(&w.at(agents(), agent)->rank), oag(), agents(),
+                                   g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT), last, last_scan);
+              if (last != INVALID) {
+                scanning = last_scan != 0u;
+                if (last_scan) scan_start = Cursor{c.leaf, last, 0u};
+              }
+              if (f >= nn) {  // no event in this leaf: on to the next one
+                c.idx = nn - 1u;
+                if (!next_entry(c)) return ST_NONTERMINATING;
+                continue;
+              }
+              c.idx = f;
+            }
+          }
+          first_step = 0;
           u32 other_order;
           if (!get_item(c, other_order)) break;
           if (other_order == item.orr) break;
@@ -1880,7 +1935,7 @@ struct Replayer {
       u32 k = rec_kind(o);
       ins = k == REC_RINS;
       if (gen_form) {
-        u32 ok = (h.w0 == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
+        u32 ok = ((h.w0 & ~(1u << RTXN_DEL_BIT)) == ((REC_RTXN << 28) | 1u)) & ((h.w1 >> 16) == 1u) & (h.w3 == l) & (l - 1u < 0xFFFFu) &
                  (pr.w0 == (REC_RPARENT << 28)) & (pr.w1 == agent) & (pr.w2 == seq - 1u) & (ins | (k == REC_RDEL));
         if (!ok) return 0;
       } else if (l == 0u) {
@@ -2138,7 +2193,7 @@ struct Replayer {
         bool remote = ((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u;
         if (kind == REC_RC) { expand_rc(h, h, gop, gpar); inl = 1; }
         if (kind == REC_LC) { expand_lc(h, h, gop); inl = 1; }
-        u32 nops = remote ? (h.w0 & 0x07FFFFFFu) : (h.w0 & 0x0FFFFFFFu);
+        u32 nops = remote ? (h.w0 & RTXN_NOPS_MASK) : (h.w0 & 0x0FFFFFFFu);
         consumed = inl ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, inl, gop, gpar) : ST_BAD_INPUT;
         p(F_PRE, 0u);

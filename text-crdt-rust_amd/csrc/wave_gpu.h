@@ -52,7 +52,11 @@ __device__ __forceinline__ u32 wave_or(u32 v) {
   return rdlane(v, 63);
 }
 
-template <int L>
+// HR (HBM root): the root level for documents past the LDS root's capacity (ROOT_CAP_MAX
+// groups): LDS holds a top level of rows (row id, groups, visible count) and the groups live in
+// 64-slot rows in HBM (block id, slot count, visible count), with gsob[block] = row << 6 | slot.
+// The replay sees the same flat group indices either way (root_* below).
+template <int L, bool HR = false>
 struct WaveGPU {
   // The lane id, computed once; lane() hands out a copy at every use (volatile: never hoisted).  A
   // hoisted lane id lets the compiler hoist every lane-derived constant (l | 32, l - 1, l * 16 ...)
@@ -128,6 +132,16 @@ struct WaveGPU {
   typedef __attribute__((address_space(3))) u32 lds_u32;  // ds_read/ds_write, never flat
   lds_u32* rt = nullptr;
   u32 rcap = 0;
+  u32* hrow = nullptr;  // HR: this document's rows (192 u32 each: blk[64], cnt[64], vis[64])
+  u32* gsob = nullptr;  // HR: block -> row << 6 | slot
+  __device__ __forceinline__ void bind_root(const Pools& P, const DocSeg& sg) {
+    if constexpr (HR) {
+      hrow = P.hrows + sg.hrow_base * (u64)HROOT_ROW;
+      gsob = P.gsob + sg.blk_base;
+    } else {
+      (void)P; (void)sg;
+    }
+  }
 
   // ---- scalar memory helpers (every lane touches the same address: uniform results, and a
   //      store is then visible to every lane's later loads by per-thread program order)
@@ -181,6 +195,18 @@ struct WaveGPU {
     }
     for (u32 k = l; k < n; k += 64) p[k] = v;
   }
+  // lane-parallel fill of n u16 (the order -> agent map)
+  __device__ __forceinline__ void fill16(u16* p, u32 n, u32 v) const {
+    u32 l = lane();
+    if (n == 0u) return;
+    if (n <= 64u) {  // one store, lanes >= n repeating item n - 1
+      u32 m = n - 1u;
+      p[l < m ? l : m] = (u16)v;
+      return;
+    }
+    for (u32 k = l; k < n; k += 64) p[k] = (u16)v;
+  }
+  __device__ __forceinline__ u32 ld16(const u16* p) const { return uni((u32)*p); }
   __device__ __forceinline__ void zero_leaf(Span* p, u32 n) const {
     u32 l = lane();
     if (l < n) *(uint4*)(p + l) = make_uint4(0, 0, 0, 0);
@@ -318,6 +344,33 @@ struct WaveGPU {
     el = in ? s.ol : el;
     er = in ? s.orr : er;
     en = in ? s.len : en;
+  }
+  // integrate's scan (replay_core.h apply_txn M_INS) over entries [a, n) of the cached leaf, each
+  // at its start: entry j's item is eo_j, its origin_left el_j.  Lane j: stop = its item is the
+  // new item's origin_right; eq = its origin_left is the new item's (X); then the name tie-break
+  // with the rank of the agent of its first order (order -> agent map, agents table):
+  // my_rank > rank: scanning = false and go on; else break if its origin_right is the new item's,
+  // else scanning from it.  Returns the first lane with an event (a break, or an origin_left
+  // other than X: a cursor compare) or n; `last` = the last lane before it (INVALID if none),
+  // `last_scan` = whether it left scanning on.
+  __device__ __forceinline__ u32 scan_batch(u32 a, u32 n, u32 X, u32 orr, u32 my_rank, const u16* oag,
+                                            const AgentRec* agents, u32 tkey, u32 tlen, u32 tagent, u32& last,
+                                            u32& last_scan) const {
+    // (the replay's register budget is spent: per-lane values are transient, the per-lane tests
+    // become lane masks at once, and the rest is scalar mask arithmetic)
+    u32 l = lane();
+    u32 o = (l >= a && l < n) ? (u32)eo : rdlane(eo, a);  // (lanes outside read a valid order's entry)
+    u32 ag = *(const u16*)((const char*)oag + (u64)(o * 2u));
+    ag = o - tkey < tlen ? tagent : ag;  // the client_with_order tail run is not in the map yet
+    u32 rk = *(const u32*)((const char*)agents + (u64)(ag * 16u + 12u));  // AgentRec::rank
+    u64 lt = ballot(my_rank > rk);
+    u64 ev = ballot(eo == orr) | ballot(el != X) | (~lt & ballot(er == orr));
+    u64 in = (n >= 64u ? ~0ull : ((1ull << n) - 1ull)) & (~0ull << a);
+    ev &= in;
+    u32 f = ev ? (u32)__builtin_ctzll(ev) : n;
+    last = f > a ? f - 1u : INVALID;
+    last_scan = f > a ? (u32)((~lt >> (f - 1u)) & 1ull) : 0u;
+    return f;
   }
   // the visible entries among lanes [a, b), as a lane mask
   __device__ __forceinline__ u64 vis_lanes(u32 a, u32 b) const { u32 l = lane(); return ballot(l >= a && l < b && en > 0); }
@@ -556,7 +609,7 @@ struct WaveGPU {
     bool ok;
     if (remote) {
       u32 ps = shfl(Z, r == 2u ? l - 2u : l - 3u);  // previous header / previous op / own header
-      bool okh = X == ((REC_RTXN << 28) | 1u) && Y == (agent | (1u << 16)) && Z == ps + 1u && Q == 1u;
+      bool okh = X == ((REC_RTXN << 28) | (1u << RTXN_DEL_BIT) | 1u) && Y == (agent | (1u << 16)) && Z == ps + 1u && Q == 1u;
       bool oko = X == ((REC_RDEL << 28) | 1u) && Y == agent && Z == ps + delta;
       bool okp = X == (REC_RPARENT << 28) && Y == agent && Z == ps - 1u;
       ok = r == 0u ? okh : (r == 1u ? oko : okp);
@@ -599,100 +652,372 @@ struct WaveGPU {
     }
   }
 
-  // ---------------------------------------------------------------- directory root (LDS)
-  // Group g of the root: rblk()[g], rcnt()[g], rvis()[g]; rcap groups per array (a multiple of
-  // 64, chosen per launch).  Sweeps go 64 groups at a time, one group per lane.
+  // ---------------------------------------------------------------- directory root
+  // Flat LDS root (!HR): group g of the root: rblk()[g], rcnt()[g], rvis()[g]; rcap groups per
+  // array (a multiple of 64, chosen per launch).  Sweeps go 64 groups at a time, one per lane.
+  // Two-level root (HR): top entry t in LDS: trow()[t], tcnt()[t], tvis()[t] (rcap entries), the
+  // top count and the row count in two more LDS words; rows in HBM.  Flat group g is slot j of the
+  // row of top entry t, where t is the first entry whose cumulative group count exceeds g.
   __device__ __forceinline__ lds_u32* rblk() const { return rt; }
   __device__ __forceinline__ lds_u32* rcnt() const { return rt + rcap; }
   __device__ __forceinline__ lds_u32* rvis() const { return rt + 2 * rcap; }
-  // Groups [ng, rcap) hold block id INVALID (no block has that id), so root_find_blk needs no
-  // bounds test; the root only grows while a wave runs (root_insert writes at most up to ng).
-  __device__ __forceinline__ void root_clear_from(u32 ng) {
-    for (u32 i = lane(); i < rcap; i += 64)
-      if (i >= ng) rblk()[i] = INVALID;
-  }
-  __device__ __forceinline__ void root_init(u32 blk, u32 cnt, u32 vis) {
-    root_clear_from(1u);
-    rblk()[0] = blk;  // every lane stores the same value: no branch
-    rcnt()[0] = cnt;
-    rvis()[0] = vis;
-  }
-  __device__ __forceinline__ void root_load(const GroupRec* g, u32 ng) {
-    root_clear_from(ng);
-    for (u32 i = lane(); i < ng; i += 64) {
-      uint4 x = *(const uint4*)(g + i);
-      rblk()[i] = x.x;
-      rcnt()[i] = x.y;
-      rvis()[i] = x.z;
-    }
-  }
-  __device__ __forceinline__ void root_store(GroupRec* g, u32 ng) const {
-    for (u32 i = lane(); i < ng; i += 64) *(uint4*)(g + i) = make_uint4(rblk()[i], rcnt()[i], rvis()[i], 0);
-  }
-  __device__ __forceinline__ u32 root_blk(u32 g) const { return uni(rblk()[g]); }
-  __device__ __forceinline__ u32 root_cnt(u32 g) const { return uni(rcnt()[g]); }
-  __device__ __forceinline__ u32 root_vis(u32 g) const { return uni(rvis()[g]); }
-  __device__ __forceinline__ u32 root_find_blk(u32 ng, u32 blk) const {
-    u32 l = lane();
-    for (u32 r = 0; r < ng; r += 64) {
+  __device__ __forceinline__ lds_u32* trow() const { return rt; }
+  __device__ __forceinline__ lds_u32* tcnt() const { return rt + rcap; }
+  __device__ __forceinline__ lds_u32* tvis() const { return rt + 2 * rcap; }
+  __device__ __forceinline__ u32 ntop() const { return uni(rt[3 * rcap]); }
+  __device__ __forceinline__ void set_ntop(u32 v) const { rt[3 * rcap] = v; }
+  __device__ __forceinline__ u32 nrows() const { return uni(rt[3 * rcap + 1]); }
+  __device__ __forceinline__ void set_nrows(u32 v) const { rt[3 * rcap + 1] = v; }
+  __device__ __forceinline__ u32* hb(u32 row) const { return hrow + (u64)row * 192u; }
+  __device__ __forceinline__ u32* hc(u32 row) const { return hrow + (u64)row * 192u + 64u; }
+  __device__ __forceinline__ u32* hv(u32 row) const { return hrow + (u64)row * 192u + 128u; }
+  // HR: top entry t of flat group g (g < the group count) and its slot j; INVALID past the end.
+  // cbefore / vbefore: groups / visible items in the top entries before t.
+  __device__ __forceinline__ u32 hr_locate(u32 g, u32& j, u32& cbefore, u32& vbefore) const {
+    u32 l = lane(), cc = 0, cv = 0, nt = ntop();
+    for (u32 r = 0; r < nt; r += 64) {
       u32 i = r + l;
-      u32 b = rblk()[i];  // i < rcap (a multiple of 64): always inside this wave's LDS slice
-      u64 m = ballot(b == blk);  // (groups >= ng hold INVALID: root_clear_from)
-      if (m) return r + (u32)__builtin_ctzll(m);
+      bool valid = i < nt;
+      u32 c = valid ? (u32)tcnt()[i] : 0u, v = valid ? (u32)tvis()[i] : 0u;
+      u32 ic = wave_incl_scan(c) + cc, iv = wave_incl_scan(v) + cv;
+      u32 k = __popcll(ballot(ic <= g));  // (invalid lanes add 0: counted only if k >= nvalid)
+      u32 nvalid = nt - r < 64u ? nt - r : 64u;
+      if (k < nvalid) {
+        cbefore = rdlane(ic, k) - rdlane(c, k);
+        vbefore = rdlane(iv, k) - rdlane(v, k);
+        j = g - cbefore;
+        return r + k;
+      }
+      cc = rdlane(ic, 63);
+      cv = rdlane(iv, 63);
     }
     return INVALID;
   }
+  // HR: top entry of a row, with the groups / visible items before it
+  __device__ __forceinline__ u32 hr_top_of_row(u32 row, u32& cbefore, u32& vbefore) const {
+    u32 l = lane(), cc = 0, cv = 0, nt = ntop();
+    for (u32 r = 0; r < nt; r += 64) {
+      u32 i = r + l;
+      bool valid = i < nt;
+      u32 tr = valid ? (u32)trow()[i] : INVALID;
+      u32 c = valid ? (u32)tcnt()[i] : 0u, v = valid ? (u32)tvis()[i] : 0u;
+      u32 ic = wave_incl_scan(c) + cc, iv = wave_incl_scan(v) + cv;
+      u64 m = ballot(tr == row);
+      if (m) {
+        u32 k = (u32)__builtin_ctzll(m);
+        cbefore = rdlane(ic, k) - rdlane(c, k);
+        vbefore = rdlane(iv, k) - rdlane(v, k);
+        return r + k;
+      }
+      cc = rdlane(ic, 63);
+      cv = rdlane(iv, 63);
+    }
+    return INVALID;
+  }
+  // HR: insert top entry (row, cnt, vis) at t, shifting [t, ntop) up (as root_insert below)
+  __device__ __forceinline__ void hr_top_insert(u32 t, u32 row, u32 cnt, u32 vis) {
+    u32 l = lane(), nt = ntop();
+    for (i32 r = (i32)(nt & ~63u); r >= (i32)(t & ~63u); r -= 64) {
+      u32 i = (u32)r + l;
+      u32 jj = i > 0u ? i - 1u : 0u;
+      u32 b = trow()[jj], c = tcnt()[jj], v = tvis()[jj];
+      __builtin_amdgcn_wave_barrier();
+      if (i > t && i <= nt) { trow()[i] = b; tcnt()[i] = c; tvis()[i] = v; }
+      __builtin_amdgcn_wave_barrier();
+    }
+    trow()[t] = row;
+    tcnt()[t] = cnt;
+    tvis()[t] = vis;
+    __builtin_amdgcn_wave_barrier();
+    set_ntop(nt + 1u);
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // Groups [ng, rcap) hold block id INVALID (no block has that id), so root_find_blk needs no
+  // bounds test; the root only grows while a wave runs (root_insert writes at most up to ng).
+  __device__ __forceinline__ void root_clear_from(u32 ng) {
+    if constexpr (HR) {
+      (void)ng;
+    } else {
+      for (u32 i = lane(); i < rcap; i += 64)
+        if (i >= ng) rblk()[i] = INVALID;
+    }
+  }
+  __device__ __forceinline__ void root_init(u32 blk, u32 cnt, u32 vis) {
+    if constexpr (HR) {
+      trow()[0] = 0u;
+      tcnt()[0] = 1u;
+      tvis()[0] = vis;
+      set_ntop(1u);
+      set_nrows(1u);
+      *hb(0) = blk;
+      *hc(0) = cnt;
+      *hv(0) = vis;
+      gsob[blk] = 0u;
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      root_clear_from(1u);
+      rblk()[0] = blk;  // every lane stores the same value: no branch
+      rcnt()[0] = cnt;
+      rvis()[0] = vis;
+    }
+  }
+  __device__ __forceinline__ void root_load(const GroupRec* g, u32 ng) {
+    if constexpr (HR) {
+      // rows of 32 groups (half full: room to insert before a row splits)
+      u32 nr = (ng + 31u) / 32u;
+      for (u32 i = lane(); i < ng; i += 64) {
+        uint4 x = *(const uint4*)(g + i);
+        u32 r = i >> 5, s = i & 31u;
+        hb(r)[s] = x.x;
+        hc(r)[s] = x.y;
+        hv(r)[s] = x.z;
+        gsob[x.x] = (r << 6) | s;
+      }
+      for (u32 t = lane(); t < nr; t += 64) {
+        u32 c = ng - 32u * t < 32u ? ng - 32u * t : 32u, v = 0;
+        for (u32 k = 0; k < c; k++) v += g[32u * t + k].vis;
+        trow()[t] = t;
+        tcnt()[t] = c;
+        tvis()[t] = v;
+      }
+      __builtin_amdgcn_wave_barrier();
+      set_ntop(nr);
+      set_nrows(nr);
+      __builtin_amdgcn_wave_barrier();
+    } else {
+      root_clear_from(ng);
+      for (u32 i = lane(); i < ng; i += 64) {
+        uint4 x = *(const uint4*)(g + i);
+        rblk()[i] = x.x;
+        rcnt()[i] = x.y;
+        rvis()[i] = x.z;
+      }
+    }
+  }
+  __device__ __forceinline__ void root_store(GroupRec* g, u32 ng) const {
+    if constexpr (HR) {
+      (void)ng;
+      u32 nt = ntop(), base = 0, l = lane();
+      for (u32 t = 0; t < nt; t++) {
+        u32 row = uni(trow()[t]), c = uni(tcnt()[t]);
+        if (l < c) *(uint4*)(g + base + l) = make_uint4(hb(row)[l], hc(row)[l], hv(row)[l], 0);
+        base += c;
+      }
+    } else {
+      for (u32 i = lane(); i < ng; i += 64) *(uint4*)(g + i) = make_uint4(rblk()[i], rcnt()[i], rvis()[i], 0);
+    }
+  }
+  __device__ __forceinline__ u32 root_blk(u32 g) const {
+    if constexpr (HR) {
+      u32 j, cb, vb;
+      u32 t = hr_locate(g, j, cb, vb);
+      return ld(hb(uni(trow()[t])) + j);
+    } else {
+      return uni(rblk()[g]);
+    }
+  }
+  __device__ __forceinline__ u32 root_cnt(u32 g) const {
+    if constexpr (HR) {
+      u32 j, cb, vb;
+      u32 t = hr_locate(g, j, cb, vb);
+      return ld(hc(uni(trow()[t])) + j);
+    } else {
+      return uni(rcnt()[g]);
+    }
+  }
+  __device__ __forceinline__ u32 root_vis(u32 g) const {
+    if constexpr (HR) {
+      u32 j, cb, vb;
+      u32 t = hr_locate(g, j, cb, vb);
+      return ld(hv(uni(trow()[t])) + j);
+    } else {
+      return uni(rvis()[g]);
+    }
+  }
+  __device__ __forceinline__ u32 root_find_blk(u32 ng, u32 blk) const {
+    if constexpr (HR) {
+      (void)ng;
+      u32 s = ld(gsob + blk), cb, vb;
+      u32 t = hr_top_of_row(s >> 6, cb, vb);
+      return t == INVALID ? INVALID : cb + (s & 63u);
+    } else {
+      u32 l = lane();
+      for (u32 r = 0; r < ng; r += 64) {
+        u32 i = r + l;
+        u32 b = rblk()[i];  // i < rcap (a multiple of 64): always inside this wave's LDS slice
+        u64 m = ballot(b == blk);  // (groups >= ng hold INVALID: root_clear_from)
+        if (m) return r + (u32)__builtin_ctzll(m);
+      }
+      return INVALID;
+    }
+  }
+  // the visible count of block blk's group += delta
+  __device__ __forceinline__ void root_add_vis_blk(u32 ng, u32 blk, u32 delta) {
+    if constexpr (HR) {
+      (void)ng;
+      u32 s = ld(gsob + blk), cb, vb;
+      u32 row = s >> 6;
+      u32 t = hr_top_of_row(row, cb, vb);
+      u32* p = hv(row) + (s & 63u);
+      *p = ld(p) + delta;
+      tvis()[t] = uni(tvis()[t]) + delta;
+    } else {
+      root_add_vis(root_find_blk(ng, blk), delta);
+    }
+  }
   __device__ __forceinline__ void root_add_vis(u32 g, u32 delta) {
-    u32 v = uni(rvis()[g]) + delta;
-    rvis()[g] = v;
+    if constexpr (HR) {
+      u32 j, cb, vb;
+      u32 t = hr_locate(g, j, cb, vb);
+      u32* p = hv(uni(trow()[t])) + j;
+      *p = ld(p) + delta;
+      tvis()[t] = uni(tvis()[t]) + delta;
+    } else {
+      u32 v = uni(rvis()[g]) + delta;
+      rvis()[g] = v;
+    }
   }
   __device__ __forceinline__ void root_set(u32 g, u32 blk, u32 cnt, u32 vis) {
-    rblk()[g] = blk;
-    rcnt()[g] = cnt;
-    rvis()[g] = vis;
+    if constexpr (HR) {
+      u32 j, cb, vb;
+      u32 t = hr_locate(g, j, cb, vb);
+      u32 row = uni(trow()[t]);
+      u32 old = ld(hv(row) + j);
+      hb(row)[j] = blk;
+      hc(row)[j] = cnt;
+      hv(row)[j] = vis;
+      gsob[blk] = (row << 6) | j;
+      tvis()[t] = uni(tvis()[t]) + vis - old;
+    } else {
+      rblk()[g] = blk;
+      rcnt()[g] = cnt;
+      rvis()[g] = vis;
+    }
   }
   // insert a group at index g, shifting [g, ng) up by one: 64-group chunks from the top down, each
   // read completely before it is written (a chunk's lane 0 reads the top of the chunk below,
-  // which is written only afterwards)
+  // which is written only afterwards).  HR: a 64-lane shift inside the group's row; a full row
+  // splits first (its upper 32 groups move to a new row linked after it in the top level).
   __device__ __forceinline__ void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
-    u32 l = lane();
-    for (i32 r = (i32)(ng & ~63u); r >= (i32)(g & ~63u); r -= 64) {
-      u32 i = (u32)r + l;
-      u32 jj = i > 0u ? i - 1u : 0u;
-      u32 b = rblk()[jj], c = rcnt()[jj], v = rvis()[jj];
+    if constexpr (HR) {
+      u32 l = lane(), j, cb, vb, t;
+      if (g < ng) {
+        t = hr_locate(g, j, cb, vb);
+      } else {  // append after the last group
+        t = ntop() - 1u;
+        j = uni(tcnt()[t]);
+      }
+      u32 row = uni(trow()[t]), c = uni(tcnt()[t]);
+      if (c == 64u) {  // split the row: [32, 64) -> a new row after it
+        u32 nr = nrows();
+        set_nrows(nr + 1u);
+        u32 b = hb(row)[l], cn = hc(row)[l], v = hv(row)[l];
+        u32 mv = wave_sum(l >= 32u ? v : 0u);
+        if (l >= 32u) {
+          hb(nr)[l - 32u] = b;
+          hc(nr)[l - 32u] = cn;
+          hv(nr)[l - 32u] = v;
+          gsob[b] = (nr << 6) | (l - 32u);
+        }
+        tcnt()[t] = 32u;
+        tvis()[t] = uni(tvis()[t]) - mv;
+        __builtin_amdgcn_wave_barrier();
+        hr_top_insert(t + 1u, nr, 32u, mv);
+        if (j > 32u) { t += 1u; row = nr; j -= 32u; }
+        c = 32u;
+      }
+      // slots [j, c) of the row move up one; the new group goes to slot j
+      u32 ob = hb(row)[l], oc = hc(row)[l], ov = hv(row)[l];
+      u32 sb = shfl(ob, l - 1u), sc = shfl(oc, l - 1u), sv = shfl(ov, l - 1u);
+      if (l > j && l <= c) {
+        hb(row)[l] = sb;
+        hc(row)[l] = sc;
+        hv(row)[l] = sv;
+        gsob[sb] = (row << 6) | l;
+      }
+      if (l == j) {
+        hb(row)[l] = blk;
+        hc(row)[l] = cnt;
+        hv(row)[l] = vis;
+        gsob[blk] = (row << 6) | l;
+      }
+      tcnt()[t] = c + 1u;
+      tvis()[t] = uni(tvis()[t]) + vis;
       __builtin_amdgcn_wave_barrier();
-      if (i > g && i <= ng) { rblk()[i] = b; rcnt()[i] = c; rvis()[i] = v; }
-      __builtin_amdgcn_wave_barrier();
+    } else {
+      u32 l = lane();
+      for (i32 r = (i32)(ng & ~63u); r >= (i32)(g & ~63u); r -= 64) {
+        u32 i = (u32)r + l;
+        u32 jj = i > 0u ? i - 1u : 0u;
+        u32 b = rblk()[jj], c = rcnt()[jj], v = rvis()[jj];
+        __builtin_amdgcn_wave_barrier();
+        if (i > g && i <= ng) { rblk()[i] = b; rcnt()[i] = c; rvis()[i] = v; }
+        __builtin_amdgcn_wave_barrier();
+      }
+      root_set(g, blk, cnt, vis);
     }
-    root_set(g, blk, cnt, vis);
   }
   // first group whose cumulative visible count exceeds pos
   __device__ __forceinline__ bool root_find_pos(u32 ng, u32 pos, u32& g, u32& base) const {
     u32 l = lane();
-    u32 carry = 0;
-    for (u32 r = 0; r < ng; r += 64) {
-      u32 i = r + l;
-      bool valid = i < ng;
-      u32 xv = rvis()[i];
-      u32 x = valid ? xv : 0u;
-      u32 incl = wave_incl_scan(x) + carry;
-      u32 nvalid = ng - r < 64 ? ng - r : 64;
-      u32 k = __popcll(ballot(incl <= pos));  // (invalid lanes add 0: counted only if k >= nvalid)
-      if (k < nvalid) {
-        g = r + k;
-        base = rdlane(incl, k) - rdlane(x, k);
-        return true;
+    if constexpr (HR) {
+      (void)ng;
+      u32 cc = 0, cv = 0, nt = ntop();
+      for (u32 r = 0; r < nt; r += 64) {
+        u32 i = r + l;
+        bool valid = i < nt;
+        u32 c = valid ? (u32)tcnt()[i] : 0u, v = valid ? (u32)tvis()[i] : 0u;
+        u32 ic = wave_incl_scan(c) + cc, iv = wave_incl_scan(v) + cv;
+        u32 k = __popcll(ballot(iv <= pos));
+        u32 nvalid = nt - r < 64u ? nt - r : 64u;
+        if (k < nvalid) {
+          u32 t = r + k, cb = rdlane(ic, k) - rdlane(c, k), vb = rdlane(iv, k) - rdlane(v, k);
+          u32 row = uni(trow()[t]), n = uni(tcnt()[t]);
+          u32 x = l < n ? hv(row)[l] : 0u;
+          u32 incl = wave_incl_scan(x) + vb;
+          u32 s = __popcll(ballot(incl <= pos));  // < n: the top entry's groups hold pos
+          g = cb + s;
+          base = rdlane(incl, s) - rdlane(x, s);
+          return true;
+        }
+        cc = rdlane(ic, 63);
+        cv = rdlane(iv, 63);
       }
-      carry = rdlane(incl, 63);
+      return false;
+    } else {
+      u32 carry = 0;
+      for (u32 r = 0; r < ng; r += 64) {
+        u32 i = r + l;
+        bool valid = i < ng;
+        u32 xv = rvis()[i];
+        u32 x = valid ? xv : 0u;
+        u32 incl = wave_incl_scan(x) + carry;
+        u32 nvalid = ng - r < 64 ? ng - r : 64;
+        u32 k = __popcll(ballot(incl <= pos));  // (invalid lanes add 0: counted only if k >= nvalid)
+        if (k < nvalid) {
+          g = r + k;
+          base = rdlane(incl, k) - rdlane(x, k);
+          return true;
+        }
+        carry = rdlane(incl, 63);
+      }
+      return false;
     }
-    return false;
   }
 
   // visible items in the groups before g (probe: Cursor::count_pos)
   __device__ __forceinline__ u32 root_vis_before(u32 g) const {
     u32 l = lane(), t = 0;
-    for (u32 r = 0; r < g; r += 64) t += wave_sum(r + l < g ? (u32)rvis()[r + l] : 0u);
-    return t;
+    if constexpr (HR) {
+      u32 j, cb, vb;
+      u32 te = hr_locate(g, j, cb, vb);
+      u32 row = uni(trow()[te]);
+      return vb + wave_sum(l < j ? (u32)hv(row)[l] : 0u);
+    } else {
+      for (u32 r = 0; r < g; r += 64) t += wave_sum(r + l < g ? (u32)rvis()[r + l] : 0u);
+      return t;
+    }
   }
 
   // ---------------------------------------------------------------- directory blocks (HBM)
