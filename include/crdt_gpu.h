@@ -81,8 +81,9 @@ int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const cha
  * the bytes [name_off[i], name_off[i+1]) of `bytes` (any bytes, not NUL-terminated).  Ids are
  * identical to crdt_agent_intern on the same call.  rank_out (optional): each name's rank among
  * the document's names in byte-lexicographic order (Rust str Ord; the order the integrate
- * tie-break compares, doc.rs:207), INVALID for "ROOT".  At most 1024 names per document
- * (CRDT_E_ARG beyond). */
+ * tie-break compares, doc.rs:207), INVALID for "ROOT".  Up to 65,534 names per document (AgentId is
+ * u16, doc.rs:66-80; CRDT_E_ARG beyond): documents with at most 1,024 names intern in an LDS table,
+ * larger ones again with the table in HBM and ranks from a sort. */
 int crdt_agent_intern_dev(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint64_t* name_off,
                           const char* bytes, uint16_t* agent_out, uint32_t* rank_out);
 

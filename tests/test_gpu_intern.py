@@ -15,27 +15,24 @@ INVALID = 0xFFFFFFFF
 
 def reference(calls):
     """calls: list of (docs, names) batches -> per batch (ids, ranks) by the reference rule."""
-    tables = {}
+    tables, index = {}, {}
     out = []
     for docs, names in calls:
         ids = []
         for d, n in zip(docs, names):
             b = n.encode() if isinstance(n, str) else bytes(n)
             t = tables.setdefault(d, [])
+            ix = index.setdefault(d, {})
             if b == b"ROOT":
                 ids.append(ROOT)
-            elif b in t:
-                ids.append(t.index(b))
+            elif b in ix:
+                ids.append(ix[b])
             else:
                 t.append(b)
+                ix[b] = len(t) - 1
                 ids.append(len(t) - 1)
-        ranks = []
-        for d, n, i in zip(docs, names, ids):
-            if i == ROOT:
-                ranks.append(INVALID)
-            else:
-                srt = sorted(tables[d])
-                ranks.append(srt.index(tables[d][i]))
+        rank_of = {d: {b: r for r, b in enumerate(sorted(t))} for d, t in tables.items()}
+        ranks = [INVALID if i == ROOT else rank_of[d][tables[d][i]] for d, i in zip(docs, ids)]
         out.append((np.array(ids, np.uint16), np.array(ranks, np.uint32)))
     return out
 
@@ -80,12 +77,35 @@ def test_intern_arbitrary_bytes_and_one_document_many_names():
     assert np.array_equal(gid, wid) and np.array_equal(grank, wrank)
 
 
-def test_intern_rejects_more_than_1024_names():
+def test_intern_past_the_lds_table():
+    # documents with more than the LDS table's 1,024 names intern with the table in HBM and ranks
+    # from a sort (k_intern_big); ids and ranks as the reference's, in the same call as small
+    # documents, and tables persist across calls
+    rng = np.random.default_rng(5)
+    e, h = _engine(3), _engine(3)
+    calls = []
+    for step in range(2):
+        big = ["u%06d-%s" % (int(x), "x" * int(x % 7)) for x in rng.integers(0, 9000, 6000)]
+        small = _random_names(rng, 300)
+        docs = [1] * len(big) + [2] * len(small) + [0] * 50
+        calls.append((docs, big + small + ["ROOT", "a"] * 25))
+    for (docs, names), (wid, wrank) in zip(calls, reference(calls)):
+        gid, grank = e.agent_intern_dev(docs, names)
+        assert np.array_equal(gid, wid)
+        assert np.array_equal(grank, wrank)
+        assert np.array_equal(h.agent_intern(docs, names), gid)
+
+
+def test_intern_rejects_more_than_u16_agents():
+    # AgentId is u16 (doc.rs:66-80): 65,534 names fit (0xFFFF is ROOT, 0xFFFE unknown), more do not
     import crdt_amd
     e = _engine(2)
-    names = ["x%05d" % i for i in range(1100)]
+    names = ["x%06d" % i for i in range(65534)]
+    gid, grank = e.agent_intern_dev([1] * len(names), names)
+    assert np.array_equal(gid, np.arange(65534, dtype=np.uint16))
+    assert np.array_equal(grank, np.arange(65534, dtype=np.uint32))  # (already in byte order)
     with pytest.raises(crdt_amd.CrdtError):
-        e.agent_intern_dev([1] * len(names), names)
+        e.agent_intern_dev([1], ["one more"])
 
 
 def test_interned_agent_replays_like_the_host_interned_one():

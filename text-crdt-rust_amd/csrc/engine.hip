@@ -1132,9 +1132,29 @@ int crdt_agent_intern_dev(crdt_engine* e, uint64_t n, const uint32_t* doc, const
   HIPCHK(hipMemcpyAsync(gn.data(), d_n, ng * 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipMemcpyAsync(gst.data(), d_st, ng * 4, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  // documents past the LDS table's INTERN_MAX names: again with the table in HBM (k_intern_big)
+  std::vector<u32> big;
+  for (u32 g = 0; g < ng; g++)
+    if (gst[g] != 0) big.push_back(g);
+  if (!big.empty()) {
+    u32* d_big = nullptr;
+    u32* d_scr = nullptr;
+    HIPCHK(dalloc(d_big, big.size()));
+    HIPCHK(dalloc(d_scr, big.size() * INTERN_BIG_SCRATCH));
+    HIPCHK(hipMemcpyAsync(d_big, big.data(), big.size() * 4, hipMemcpyHostToDevice, e->stream));
+    hipLaunchKernelGGL(k_intern_big, dim3((u32)big.size()), dim3(256), 0, e->stream, io, (const u32*)d_big, (u32)big.size(), d_scr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(id.data(), d_id, nr * 2, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(rank.data(), d_rank, nr * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(gn.data(), d_n, ng * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(gst.data(), d_st, ng * 4, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    dfree(d_big);
+    dfree(d_scr);
+  }
   for (u32 g = 0; g < ng; g++) {
     if (gst[g] != 0) {
-      g_last_error = "crdt_agent_intern_dev: more than 1024 distinct names in one document";
+      g_last_error = "crdt_agent_intern_dev: more than 65,534 distinct names in one document (AgentId is u16)";
       return CRDT_E_ARG;
     }
   }

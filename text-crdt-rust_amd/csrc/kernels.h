@@ -1234,6 +1234,56 @@ __device__ __forceinline__ bool intern_less(const unsigned char* b, u32 a0, u32 
   }
   return la < lc;
 }
+// One group's names -> ids by first appearance (one wave: the admission is sequential in ref
+// order, which is what makes the ids the reference's).  ht / hh: open-addressing table of
+// ht_slots (a power of two) slots, 0 = empty else id + 1, with the slot name's FNV-1a hash; rep:
+// a ref naming each id.  Returns the distinct names (k); st = -1 past max_names.
+__device__ __forceinline__ u32 intern_admit(const InternIO& io, u32 g, u32* ht, u32* hh, u32* rep, u32 ht_slots,
+                                            u32 max_names, i32& st) {
+  u32 l = threadIdx.x & 63u;
+  const unsigned char* B = io.bytes;
+  u64 r0 = io.roff[g], r1 = io.roff[g + 1];
+  u32 k = 0;
+  st = 0;
+  for (u64 c = r0; c < r1 && st == 0; c += 64) {
+    u64 r = c + l;
+    bool v = r < r1;
+    u32 a = v ? io.noff[r] : 0u, b = v ? io.noff[r + 1] : 0u;
+    u32 h = 2166136261u;
+    for (u32 i = a; i < b; i++) h = (h ^ B[i]) * 16777619u;
+    bool root = v && b - a == 4u && B[a] == 'R' && B[a + 1] == 'O' && B[a + 2] == 'O' && B[a + 3] == 'T';
+    u32 id = INVALID;
+    if (v && !root) {  // lookup
+      for (u32 s = h & (ht_slots - 1u);; s = (s + 1u) & (ht_slots - 1u)) {
+        u32 e = ht[s];
+        if (e == 0u) break;
+        if (hh[s] == h && intern_eq(B, a, b, io.noff[rep[e - 1u]], io.noff[rep[e - 1u] + 1u])) { id = e - 1u; break; }
+      }
+    }
+    u64 need = __builtin_amdgcn_ballot_w64(v && !root && id == INVALID);
+    while (need) {  // admit the chunk's new names, first appearance first
+      u32 ld = (u32)__builtin_ctzll(need);
+      u32 lh = __builtin_amdgcn_readlane(h, ld), la = __builtin_amdgcn_readlane(a, ld), lb = __builtin_amdgcn_readlane(b, ld);
+      if (k >= max_names) { st = -1; break; }
+      bool mine = (need >> l) & 1ull;
+      bool same = mine && h == lh && intern_eq(B, a, b, la, lb);
+      if (same) id = k;
+      if (l == ld) {
+        u32 s = h & (ht_slots - 1u);
+        while (ht[s] != 0u) s = (s + 1u) & (ht_slots - 1u);
+        ht[s] = k + 1u;
+        hh[s] = h;
+        rep[k] = (u32)r;
+      }
+      __threadfence_block();
+      __builtin_amdgcn_wave_barrier();
+      k++;
+      need &= ~__builtin_amdgcn_ballot_w64(same);
+    }
+    if (v) io.id[r] = (u16)(root ? ROOT_AGENT : id);
+  }
+  return k;
+}
 __global__ __launch_bounds__(64) void k_intern(InternIO io, u32 n_groups) {
   __shared__ u32 ht[INTERN_HT];      // 0 = empty, else id + 1
   __shared__ u32 hh[INTERN_HT];      // hash of the slot's name
@@ -1245,44 +1295,8 @@ __global__ __launch_bounds__(64) void k_intern(InternIO io, u32 n_groups) {
   __builtin_amdgcn_wave_barrier();
   const unsigned char* B = io.bytes;
   u64 r0 = io.roff[g], r1 = io.roff[g + 1];
-  u32 k = 0;
-  i32 st = 0;
-  for (u64 c = r0; c < r1 && st == 0; c += 64) {
-    u64 r = c + l;
-    bool v = r < r1;
-    u32 a = v ? io.noff[r] : 0u, b = v ? io.noff[r + 1] : 0u;
-    u32 h = 2166136261u;
-    for (u32 i = a; i < b; i++) h = (h ^ B[i]) * 16777619u;
-    bool root = v && b - a == 4u && B[a] == 'R' && B[a + 1] == 'O' && B[a + 2] == 'O' && B[a + 3] == 'T';
-    u32 id = INVALID;
-    if (v && !root) {  // lookup
-      for (u32 s = h & (INTERN_HT - 1u);; s = (s + 1u) & (INTERN_HT - 1u)) {
-        u32 e = ht[s];
-        if (e == 0u) break;
-        if (hh[s] == h && intern_eq(B, a, b, io.noff[rep[e - 1u]], io.noff[rep[e - 1u] + 1u])) { id = e - 1u; break; }
-      }
-    }
-    u64 need = __builtin_amdgcn_ballot_w64(v && !root && id == INVALID);
-    while (need) {  // admit the chunk's new names, first appearance first
-      u32 ld = (u32)__builtin_ctzll(need);
-      u32 lh = __builtin_amdgcn_readlane(h, ld), la = __builtin_amdgcn_readlane(a, ld), lb = __builtin_amdgcn_readlane(b, ld);
-      if (k >= INTERN_MAX) { st = -1; break; }
-      bool mine = (need >> l) & 1ull;
-      bool same = mine && h == lh && intern_eq(B, a, b, la, lb);
-      if (same) id = k;
-      if (l == ld) {
-        u32 s = h & (INTERN_HT - 1u);
-        while (ht[s] != 0u) s = (s + 1u) & (INTERN_HT - 1u);
-        ht[s] = k + 1u;
-        hh[s] = h;
-        rep[k] = (u32)r;
-      }
-      __builtin_amdgcn_wave_barrier();
-      k++;
-      need &= ~__builtin_amdgcn_ballot_w64(same);
-    }
-    if (v) io.id[r] = (u16)(root ? ROOT_AGENT : id);
-  }
+  i32 st;
+  u32 k = intern_admit(io, g, ht, hh, rep, INTERN_HT, INTERN_MAX, st);
   __builtin_amdgcn_wave_barrier();
   // ranks: names smaller than each distinct name (lane per name)
   for (u32 i = l; i < k; i += 64) {
@@ -1301,6 +1315,67 @@ __global__ __launch_bounds__(64) void k_intern(InternIO io, u32 n_groups) {
   if (l == 0) {
     io.n_out[g] = k;
     io.status[g] = st;
+  }
+}
+
+// Groups past INTERN_MAX distinct names (a document with more agents than the LDS table holds;
+// the reference allows 65,535, AgentId = u16): the same admission with the table in HBM scratch,
+// and ranks from a block-wide bitonic sort of the names (byte-lexicographic) instead of k^2
+// counting.  Block (256 threads) per listed group; scratch per block: INTERN_BIG_HT slots x 2 +
+// INTERN_BIG_MAX x 3 u32.
+constexpr u32 INTERN_BIG_MAX = 65534, INTERN_BIG_HT = 1u << 17, INTERN_BIG_SORT = 1u << 16;
+constexpr u64 INTERN_BIG_SCRATCH = 2ull * INTERN_BIG_HT + 3ull * INTERN_BIG_SORT;  // u32 per group
+__global__ __launch_bounds__(256) void k_intern_big(InternIO io, const u32* groups, u32 n, u32* scratch) {
+  if (blockIdx.x >= n) return;
+  u32 g = groups[blockIdx.x], t = threadIdx.x;
+  u32* ht = scratch + (u64)blockIdx.x * INTERN_BIG_SCRATCH;
+  u32* hh = ht + INTERN_BIG_HT;
+  u32* rep = hh + INTERN_BIG_HT;
+  u32* rk = rep + INTERN_BIG_SORT;
+  u32* srt = rk + INTERN_BIG_SORT;
+  for (u32 i = t; i < INTERN_BIG_HT; i += 256) ht[i] = 0u;
+  __syncthreads();
+  __shared__ u32 sk;
+  __shared__ i32 sst;
+  if (t < 64) {
+    i32 st;
+    u32 k = intern_admit(io, g, ht, hh, rep, INTERN_BIG_HT, INTERN_BIG_MAX, st);
+    if (t == 0) { sk = k; sst = st; }
+  }
+  __syncthreads();
+  u32 k = sk;
+  const unsigned char* B = io.bytes;
+  u32 P = 1;
+  while (P < k) P <<= 1;
+  for (u32 i = t; i < P; i += 256) srt[i] = i < k ? i : INVALID;
+  __syncthreads();
+  auto less = [&](u32 x, u32 y) -> bool {  // INVALID (padding) sorts last
+    if (y == INVALID) return x != INVALID;
+    if (x == INVALID) return false;
+    u32 rx = rep[x], ry = rep[y];
+    return intern_less(B, io.noff[rx], io.noff[rx + 1], io.noff[ry], io.noff[ry + 1]);
+  };
+  for (u32 size = 2; size <= P; size <<= 1) {
+    for (u32 stride = size >> 1; stride > 0; stride >>= 1) {
+      for (u32 i = t; i < P / 2; i += 256) {
+        u32 lo = 2 * i - (i & (stride - 1)), hi = lo + stride;  // pair (lo, hi) of this step
+        bool up = (lo & size) == 0;
+        u32 x = srt[lo], y = srt[hi];
+        if (less(y, x) == up) { srt[lo] = y; srt[hi] = x; }
+      }
+      __syncthreads();
+    }
+  }
+  for (u32 i = t; i < k; i += 256) rk[srt[i]] = i;
+  __syncthreads();
+  u64 r0 = io.roff[g], r1 = io.roff[g + 1];
+  for (u64 r = r0 + t; r < r1; r += 256) {
+    u32 id = io.id[r];
+    io.rank[r] = (id == ROOT_AGENT || id >= k) ? INVALID : rk[id];
+  }
+  if (t == 0) {
+    io.n_out[g] = k;
+    io.status[g] = sst;
   }
 }
 

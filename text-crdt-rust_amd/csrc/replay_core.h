@@ -72,6 +72,10 @@ enum : u32 {
   F_PRE, PRE_ITEM, PRE_C = PRE_ITEM + 4,
   F_GEN = PRE_C + 3,  // the record being replayed is a GEN record (generated ops)
   T_RB_BASE,
+  // While F_FAST is set, the client_with_order / txns tail lengths and frontier[0] are kept as of
+  // next_order == F_BASE: fast commits only advance next_order (and the author's item_orders
+  // tail, which the fast path reads); materialize_tails() brings them up to date.
+  F_BASE,
   // x2: leaf cache bookkeeping
   C_LEAF = 128, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
@@ -86,7 +90,7 @@ enum : u32 {
 };
 static_assert(K_AGMAP < 64, "read-only slots live in the first context register");
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
-static_assert(T_RB_BASE < 128, "DocState and the flags live in the second context register");
+static_assert(F_BASE < 128, "DocState and the flags live in the second context register");
 static_assert(N_SLOTS <= 192, "three context registers");
 
 template <class W, int L>
@@ -249,7 +253,18 @@ struct Replayer {
     p(T_FR0, w.ld(fr()));
   }
   // write-back tails -> HBM (the tables' last entries; frontier[0])
+  // the tails a run of fast commits left behind next_order (F_BASE)
+  CRDT_HD void materialize_tails() {
+    if (!g(F_FAST)) return;
+    u32 no = g(S_NEXT_ORDER), d = no - g(F_BASE);
+    if (d == 0u) return;
+    inc(T_CWO_LEN, d);
+    inc(T_TX_LEN, d);
+    p(T_FR0, no - 1u);
+    p(F_BASE, no);
+  }
   CRDT_HD void flush_tails() {
+    materialize_tails();
     agent_fill_tail();
     u32 n = g(S_N_CWO);
     if (n) w.st(&w.at(cwo(), n - 1)->len, g(T_CWO_LEN));
@@ -1019,6 +1034,7 @@ struct Replayer {
 #ifdef CRDT_PROF
     u64 prof_t0 = w.clock();
 #endif
+    materialize_tails();
     p(F_FAST, 0u);  // the general path changes the tails fast_txn_ok relies on
     u32 nops, agent, np = 0, seq, txn_len;
     if (!remote) {
@@ -1299,14 +1315,14 @@ struct Replayer {
     if (g(S_N_TXN) == 0u) return 0;
     return g(T_TX_ORDER) + g(T_TX_LEN) == first;
   }
+  // (S_CAP_NEED is read by the host only after a capacity stop, which fits() records afresh)
   CRDT_HD void fast_txn_commit(u32 first, u32 len) {
+    if (!g(F_FAST)) {  // the first fast commit after the general path: the lazy tails start here
+      p(F_BASE, first);
+      p(F_FAST, 1u);
+    }
     p(S_NEXT_ORDER, first + len);
-    inc(T_CWO_LEN, len);
     inc(T_AGL_LEN, len);
-    p(T_FR0, first + len - 1u);
-    inc(T_TX_LEN, len);
-    p(S_CAP_NEED, 0u);
-    p(F_FAST, 1u);
   }
   // the first order after entry idx of the cached leaf (get_item at the entry's end, cursor.rs:233-239)
   CRDT_HD u32 next_item_after(u32 idx, u32& order) {
@@ -2054,6 +2070,7 @@ struct Replayer {
   // before it; deleted items report the position of the next visible one.  Unknown answers are
   // (0xFFFF, 0xFFFFFFFF) and (0xFFFFFFFF, 2), as the published-index queries answer.
   CRDT_HD void probe(const Rec& q, u32 pos) {
+    materialize_tails();  // (order_to_loc reads the client_with_order tail)
     u32 a = 0xFFFFu, s = INVALID, ps = INVALID, dl = 2u;
     Cursor c;
     u32 o;
