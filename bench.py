@@ -301,6 +301,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="target length of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-text", action="store_true", help="skip the text materialisation leg")
+    ap.add_argument("--host-intern", action="store_true",
+                    help="intern the per-document client names on the host (default: k_intern on the GPU)")
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
     ap.add_argument("--rehearse-cpu", action="store_true", help="CPU/gloo rehearsal of the multi-rank plumbing")
     args = ap.parse_args()
@@ -339,6 +341,7 @@ def main():
     names = [doc_name(doc0 + i) for i in range(n)]
     # the wire's name table: index 0 is "jeremy" (the trace author); replace it per document
     eng = crdt_amd.Engine(n, 32, device=local_rank if world > 1 else 0)
+    eng.device_intern(not args.host_intern)  # staging's name interning: k_intern (one wave per document)
     t0 = time.time()
     eng.stage_remote_replicated(wire, 0, names)
     stage_s = time.time() - t0
@@ -463,6 +466,7 @@ def main():
             "world_size": dist.get_world_size() if dist is not None else 1,
             "per_rank_ops_s": [n_ops_doc * n * args.steps / t for t in per_rank],
             "stage_s": stage_s,
+            "stage_intern": "host" if args.host_intern else "device (k_intern)",
             "materialize": mat,
         }
         print(json.dumps(out))

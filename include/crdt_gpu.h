@@ -206,6 +206,10 @@ int crdt_fit(crdt_engine* e);
 // crdt_stage_remote_replicated) read one device copy of it instead of a copy each (records
 // are read-only input).  Off by default.
 int crdt_set_share_streams(crdt_engine* e, int on);
+// on != 0: crdt_stage_remote_replicated interns every document's authors on the device
+// (crdt_agent_intern_dev, one wave per document) instead of on the host.  Same ids either way
+// (get_or_create_agent_id, doc.rs:66-80).  Off by default.
+int crdt_set_device_intern(crdt_engine* e, int on);
 // Device bytes the engine holds (per-document pools, staged records, content, text).
 uint64_t crdt_mem_bytes(const crdt_engine* e);
 // Config 1's per-op check: after txn t (of every listed document), ask pos_to_loc(probes[t].pos)

@@ -18,7 +18,29 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--docs", type=int, default=125000)
 ap.add_argument("--names", type=int, default=16)
 ap.add_argument("--reps", type=int, default=4)
+ap.add_argument("--replicated", action="store_true",
+                help="time crdt_stage_remote_replicated (bench.py's staging: AP remote, one client name per "
+                     "document) with device vs host interning; replay both and compare digests")
 a = ap.parse_args()
+if a.replicated:
+    from crdt_amd.traces import load_remote_wire
+    wire = load_remote_wire("automerge-paper")
+    names = ["%08x-client" % ((d * 2654435761) % (1 << 32)) for d in range(a.docs)]
+    out = {"metric": "crdt_stage_remote_replicated seconds (AP remote, renamed author per document)", "docs": a.docs}
+    dg = {}
+    for mode in ("device", "host"):
+        e = crdt_amd.Engine(a.docs, 32)
+        e.device_intern(mode == "device")
+        t0 = time.perf_counter()
+        e.stage_remote_replicated(wire, 0, names)
+        out[mode + "_stage_s"] = time.perf_counter() - t0
+        st = e.run()
+        assert (st == 0).all()
+        dg[mode] = e.digests()
+        del e
+    out["parity_ok"] = bool(np.array_equal(dg["device"], dg["host"]))
+    print(json.dumps(out))
+    sys.exit(0)
 rng = np.random.default_rng(5)
 docs = np.repeat(np.arange(a.docs, dtype=np.uint32), a.names * a.reps)
 k = rng.integers(0, a.names, docs.shape[0])

@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=5_000_000)
-ap.add_argument("--docs", type=int, default=1024)
+ap.add_argument("--docs", type=int, default=512)
 ap.add_argument("--reps", type=int, default=2)
 a = ap.parse_args()
 

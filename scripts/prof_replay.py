@@ -18,9 +18,15 @@ ap.add_argument("--local", action="store_true")
 ap.add_argument("--wire", default=None, help="a .rtx.gz remote wire file instead of a trace")
 ap.add_argument("--clean", action="store_true", help="reset and replay once more (single launch)")
 ap.add_argument("--random", type=int, default=0, help="config 4: this many generated ops per document")
+ap.add_argument("--config5", action="store_true",
+                help="config 5: one seeded concurrent history (1 M-char base, 16 agents x 64 rounds x 64 txns) on every document")
 a = ap.parse_args()
 e = crdt_amd.Engine(a.docs, 32)
-if a.random:
+if a.config5:
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fuzz_gen import config5_wire
+    e.stage_remote_replicated(config5_wire(7, base_len=1 << 20, n_agents=16, rounds=64, ops=64), 0xFFFFFFFF, [""] * a.docs)
+elif a.random:
     e.stage_random(list(range(a.docs)), "gen", a.random, 0xC0FFEE)
 elif a.local:
     t = load_trace(a.trace)

@@ -13,7 +13,7 @@ import numpy as np
 
 ROOT = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 EMU_DIR = os.path.join(ROOT, "tests", "emu")
-LIB_PATH = os.path.join(EMU_DIR, "build", "libemu.so")
+LIB_PATH = os.environ.get("CRDT_EMU_LIB") or os.path.join(EMU_DIR, "build", "libemu.so")  # (env: a coverage build)
 _lib = None
 
 

@@ -122,3 +122,22 @@ def test_interned_agent_replays_like_the_host_interned_one():
     assert (e.apply_trace([1], int(gid[1]), c, p) == 0).all()
     assert (h.apply_trace([1], int(hid[1]), c, p) == 0).all()
     assert int(e.digests()[1]) == int(h.digests()[1])
+
+
+def test_replicated_staging_interns_on_the_device():
+    # crdt_stage_remote_replicated with crdt_set_device_intern: every document's authors go
+    # through k_intern in one call; ids, and so the replayed states, equal the host-interned path
+    # (renamed agent = name index 3 of a 16-agent concurrent history, so the tie-break ranks move)
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from fuzz_gen import config5_wire
+    w = config5_wire(3, base_len=2000, rounds=6, ops=4)
+    n = 24
+    names = ["c%02d-%s" % (d, "z" * (d % 5)) for d in range(n)]
+    e, h = _engine(n), _engine(n)
+    e.device_intern(True)
+    e.stage_remote_replicated(w, 3, names)
+    h.stage_remote_replicated(w, 3, names)
+    assert (e.run() == 0).all() and (h.run() == 0).all()
+    assert np.array_equal(e.digests(), h.digests())

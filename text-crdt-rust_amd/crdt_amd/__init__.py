@@ -161,6 +161,7 @@ def lib():
     L.crdt_debug_state.argtypes = [vp, u32, P(u32)]
     L.crdt_fit.argtypes = [vp]
     L.crdt_set_share_streams.argtypes = [vp, C.c_int]
+    L.crdt_set_device_intern.argtypes = [vp, C.c_int]
     L.crdt_apply_local_probed.argtypes = [vp, u64, P(u32), P(u64), vp, vp, vp, vp, P(i32)]
     L.crdt_mem_bytes.argtypes = [vp]
     L.crdt_mem_bytes.restype = u64
@@ -208,7 +209,7 @@ EXPORTED_SYMBOLS = [
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
-    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams",
+    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams", "crdt_set_device_intern",
     # include/crdt_trace.h (host-only trace ingestion)
     "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
@@ -387,6 +388,10 @@ class Engine:
     def share_streams(self, on: bool = True):
         """documents staged from the same host stream read one device copy"""
         _check(self.L.crdt_set_share_streams(self.h, int(on)), "share_streams")
+
+    def device_intern(self, on: bool = True):
+        """stage_remote_replicated interns every document's authors with k_intern (same ids)"""
+        _check(self.L.crdt_set_device_intern(self.h, int(on)), "device_intern")
 
     def mem_bytes(self) -> int:
         """device bytes held by the per-document pools + staged records"""

@@ -147,6 +147,7 @@ struct crdt_engine {
   u64 probe_cap = 0;
   bool has_probes = false;
   bool share_streams = false;  // documents staged with the same host stream read one device copy
+  bool intern_on_device = false;  // crdt_stage_remote_replicated interns through k_intern
   bool published = false;
   double last_replay_ms = 0, last_publish_ms = 0, last_materialize_ms = 0;
   // text materialisation: order-indexed content streams, per-document stream offsets, output text
@@ -1302,6 +1303,26 @@ int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t w
     for (const auto& t : wv.txns)
       if (!seen[t.agent_name]) seen[t.agent_name] = 1, authors.push_back(t.agent_name);
   }
+  if (e->intern_on_device) {
+    // Every document's authors, in order of first appearance, interned by k_intern in one call
+    // (one wave per document); the host tables are mirrored by crdt_agent_intern_dev, so the
+    // mapping check below finds every fresh document already interned.
+    std::vector<u32> ddoc;
+    std::vector<u64> off{0};
+    std::string blob;
+    ddoc.reserve(e->n_docs * authors.size());
+    for (u64 d = 0; d < e->n_docs; d++) {
+      for (u32 a : authors) {
+        const std::string& nm = (names && a == rename_idx) ? std::string(names[d]) : wv.names[a];
+        blob += nm;
+        ddoc.push_back((u32)d);
+        off.push_back(blob.size());
+      }
+    }
+    std::vector<uint16_t> out(ddoc.size());
+    int r = crdt_agent_intern_dev(e, ddoc.size(), ddoc.data(), off.data(), blob.data(), out.data(), nullptr);
+    if (r) return r;
+  }
   for (u64 d = 0; d < e->n_docs; d++) {
     ids[d] = d;
     std::vector<std::string> nm = wv.names;  // only the names differ per document
@@ -1309,7 +1330,16 @@ int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t w
     AgentTable& at = e->docs[d].agents;
     std::vector<Rec> tmp;
     bool fresh = at.names.empty();
-    if (d > 0 && fresh && !uniq.empty()) {
+    if (d > 0 && e->intern_on_device && !uniq.empty()) {
+      // (interned above: only the mapping decides whether document 0's stream fits)
+      std::vector<u32> m;
+      for (const auto& n : nm) m.push_back(at.lookup(n));
+      if (m == first_map) {
+        sp[d] = &uniq[0];
+        needs[d] = needs[0];
+        continue;
+      }
+    } else if (d > 0 && fresh && !uniq.empty()) {
       // intern in txn order (authors create, others look up) exactly as encode_remote does
       AgentTable probe = at;
       for (u32 a : authors) probe.get_or_create(nm[a]);
@@ -1409,6 +1439,12 @@ int crdt_apply_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs
 int crdt_set_share_streams(crdt_engine* e, int on) {
   if (!e) return CRDT_E_ARG;
   e->share_streams = on != 0;
+  return 0;
+}
+
+int crdt_set_device_intern(crdt_engine* e, int on) {
+  if (!e) return CRDT_E_ARG;
+  e->intern_on_device = on != 0;
   return 0;
 }
 
