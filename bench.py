@@ -305,6 +305,9 @@ def main():
                     help="intern the per-document client names on the host (default: k_intern on the GPU)")
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
     ap.add_argument("--rehearse-cpu", action="store_true", help="CPU/gloo rehearsal of the multi-rank plumbing")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the multi-rank path on one GPU: every rank runs its engine on cuda:0 and "
+                         "the collectives go over gloo (CPU tensors); not a scaling measurement")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -325,13 +328,15 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    if torch.cuda.device_count() < (world if world > 1 else 1):  # (counting devices does not initialise them)
-        print(f"bench.py: {world} rank(s) need {world} GPU(s); {torch.cuda.device_count()} visible", file=sys.stderr)
+    need = world if world > 1 and not args.share_gpu else 1
+    if torch.cuda.device_count() < need:  # (counting devices does not initialise them)
+        print(f"bench.py: {world} rank(s) need {need} GPU(s); {torch.cuda.device_count()} visible", file=sys.stderr)
         sys.exit(2)
+    gpu = 0 if args.share_gpu else local_rank
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(gpu)
+        dist.init_process_group("gloo" if args.share_gpu else "nccl")
     import crdt_amd
     from crdt_amd.traces import load_remote_wire
 
@@ -340,7 +345,7 @@ def main():
     doc0, n = shard(rank, world, args.docs)
     names = [doc_name(doc0 + i) for i in range(n)]
     # the wire's name table: index 0 is "jeremy" (the trace author); replace it per document
-    eng = crdt_amd.Engine(n, 32, device=local_rank if world > 1 else 0)
+    eng = crdt_amd.Engine(n, 32, device=gpu)
     eng.device_intern(not args.host_intern)  # staging's name interning: k_intern (one wave per document)
     t0 = time.time()
     eng.stage_remote_replicated(wire, 0, names)
@@ -357,7 +362,7 @@ def main():
     q = args.queries
     qdoc = np.repeat(np.arange(n, dtype=np.uint32), q)
     qpos = (rng.random(n * q) * np.repeat(lens, q)).astype(np.uint32)
-    dev = torch.device("cuda", local_rank if world > 1 else 0)
+    dev = torch.device("cuda", gpu)
     d_doc = torch.from_numpy(qdoc.view(np.int32)).to(dev)
     d_pos = torch.from_numpy(qpos.view(np.int32)).to(dev)
     d_ag = torch.zeros(n * q, dtype=torch.int16, device=dev)
@@ -414,7 +419,7 @@ def main():
     ok = bool((st == 0).all())
     q_ok = bool(((d_p2 == d_pos) & (d_del == 0) & (d_ag == 0)).all().item()) if q else True
     dg = eng.digests()
-    t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, dev)
+    t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, torch.device("cpu") if args.share_gpu else dev)
     gold = golden(args.trace, "remote_digest")
     gold = int(gold, 16) if gold else None
     ok = ok and q_ok and bool((all_dg == all_dg[0]).all()) and (gold is None or int(all_dg[0]) == gold)
@@ -449,7 +454,8 @@ def main():
             "data": "synthetic-from-trace: benchmark_data/automerge-paper remote form, randomised client ids",
             "config": {"workload": f"config2: {n} docs/GPU x {args.trace} remote txns ({n_ops_doc} ops/doc), "
                                    f"replay+publish+{q} pos->loc & loc->pos queries/doc",
-                       "docs_per_gpu": n, "ops_per_doc": n_ops_doc, "parallelism": f"doc-sharded x{world}",
+                       "docs_per_gpu": n, "ops_per_doc": n_ops_doc,
+                       "parallelism": f"doc-sharded x{world}" + (" (rehearsal: every rank on cuda:0, gloo)" if args.share_gpu else ""),
                        "waves_per_simd": n / SIMDS, "hbm_bytes_per_doc": mem / n},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": measured_traffic(n),

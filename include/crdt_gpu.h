@@ -210,6 +210,15 @@ int crdt_set_share_streams(crdt_engine* e, int on);
 // (crdt_agent_intern_dev, one wave per document) instead of on the host.  Same ids either way
 // (get_or_create_agent_id, doc.rs:66-80).  Off by default.
 int crdt_set_device_intern(crdt_engine* e, int on);
+/* Kernel family behind crdt_pos_to_loc_dev_async / crdt_loc_to_pos_dev_async (same answers):
+ *   CRDT_QUERY_LDS (default): 4,096-query chunks of one document stage its index in LDS and
+ *     search in lockstep;
+ *   CRDT_QUERY_PER_THREAD: one thread per query, binary searches in HBM;
+ *   CRDT_QUERY_MERGE: for batches sorted per document (pos ascending; loc->pos by (agent, seq)):
+ *     pos->loc merges each chunk against the document's visible prefix (merge path), loc->pos
+ *     searches per thread; unsorted or mixed chunks are answered per thread. */
+enum { CRDT_QUERY_LDS = 0, CRDT_QUERY_PER_THREAD = 1, CRDT_QUERY_MERGE = 2 };
+int crdt_set_query_kernel(crdt_engine* e, int mode);
 // Device bytes the engine holds (per-document pools, staged records, content, text).
 uint64_t crdt_mem_bytes(const crdt_engine* e);
 // Config 1's per-op check: after txn t (of every listed document), ask pos_to_loc(probes[t].pos)

@@ -8,8 +8,8 @@ mkdir -p gpurun_out
 TAG=${TAG:-v2}
 R="--kernel-include-regex k_replay"
 P="python scripts/prof_replay.py --docs 1024 --clean --config5"
-timeout -k 10 300 python -u scripts/bench_kevin.py > gpurun_out/kevin_$TAG.json 2> gpurun_out/kevin_$TAG.err && echo kevin-ok && \
-timeout -k 10 300 python -u scripts/bench_intern.py --replicated --docs 8192 > gpurun_out/intern_repl_$TAG.json 2>&1 && echo intern-ok && \
+
+
 DOCS=8192 bash scripts/gpu_pmc_mat.sh && \
 timeout -k 10 400 python -u scripts/bench_config5.py --docs 4096 > gpurun_out/c5_4096_$TAG.json 2> gpurun_out/c5_4096_$TAG.err && echo c5-ok && \
 timeout -s KILL 150 rocprofv3 $R --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVES SQ_INSTS_BRANCH -d gpurun_out/c5pmc1 -o pmc1 --output-format csv -- $P > gpurun_out/c5pmc1.log 2>&1 && echo pmc1-ok && \

@@ -9,16 +9,16 @@ TOP=${1:-60}
 TRACE=${2:-automerge-paper}
 mkdir -p $OUT
 CS=$ROOT/text-crdt-rust_amd/csrc
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -g -std=c++17 -fno-strict-aliasing -mllvm -phi-elim-split-all-critical-edges=1 \
+[ -n "$SKIP_DEV" ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -g -std=c++17 -fno-strict-aliasing -mllvm -phi-elim-split-all-critical-edges=1 \
   -mllvm -structurizecfg-skip-uniform-regions=1 -I$ROOT/include -I$CS --cuda-device-only --no-gpu-bundle-output -c \
   $CS/engine.hip -o $OUT/dev.o
 LB=/opt/rocm/lib/llvm/bin
-$LB/llvm-objdump -d --no-show-raw-insn $OUT/dev.o > $OUT/dis.txt
-$LB/llvm-dwarfdump --debug-info $OUT/dev.o > $OUT/dwarf.txt
-$LB/llvm-dwarfdump --debug-line $OUT/dev.o > $OUT/lines.txt
+[ -n "$SKIP_DEV" ] || $LB/llvm-objdump -d --no-show-raw-insn $OUT/dev.o > $OUT/dis.txt
+[ -n "$SKIP_DEV" ] || $LB/llvm-dwarfdump --debug-info $OUT/dev.o > $OUT/dwarf.txt
+[ -n "$SKIP_DEV" ] || $LB/llvm-dwarfdump --debug-line $OUT/dev.o > $OUT/lines.txt
 rm -rf $OUT/cov && mkdir -p $OUT/cov
 ( cd $OUT/cov && g++ -O0 --coverage -g -std=c++17 -fPIC -w -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -I$CS -I$ROOT/tests/emu \
-    -shared -o libemu_cov.so $ROOT/tests/emu/emu.cpp )
+    -c -o emu.o $ROOT/tests/emu/emu.cpp && g++ --coverage -shared -o libemu_cov.so emu.o )
 OPS=$(cd $ROOT/tests && CRDT_EMU_LIB=$OUT/cov/libemu_cov.so python -c "
 import sys; sys.path.insert(0, '$ROOT/text-crdt-rust_amd')
 from emu_lib import EmuDoc
@@ -28,5 +28,5 @@ assert e.run_wire(load_remote_wire('$TRACE'), 64) == 0
 t = load_trace('$TRACE')
 print(int(t.patches.shape[0]) if t.patches.ndim > 1 else len(t.patches) // 3)
 ")
-( cd $OUT/cov && gcov -p -o . $ROOT/tests/emu/emu.cpp > /dev/null 2>&1 || true )
+( cd $OUT/cov && gcov -o . $ROOT/tests/emu/emu.cpp > /dev/null 2>&1 || true )
 python $ROOT/scripts/isa_dynamic.py $OUT/dev.o $OUT/dis.txt $OUT/dwarf.txt $OUT/lines.txt $OUT/cov $OPS $TOP

@@ -7,6 +7,7 @@ SQ counters on gfx950 count per wave-instruction; SQ_WAVE_CYCLES / SQ_BUSY_CYCLE
 clock.  WAIT_ANY + WAIT_INST_ANY + ACTIVE_INST_ANY ~= WAVE_CYCLES (MI355X_MICROARCH.md, PMC
 slots)."""
 import csv
+import os
 import glob
 import json
 import sys
@@ -30,7 +31,7 @@ total_inst = sum(agg.get(k, 0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_I
                                          "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_FLAT"))
 wc = agg.get("SQ_WAVE_CYCLES", 0)
 res = {
-    "kernel": "k_replay<32>", "docs": docs, "ops_per_doc": ops_doc, "workload": "config 2: automerge-paper remote, one clean launch",
+    "kernel": "k_replay<32>", "docs": docs, "ops_per_doc": ops_doc, "workload": os.environ.get("SQ_WORKLOAD", "config 2: automerge-paper remote, one clean launch"),
     "launch": meta, "counters": agg,
     "per_op": {k.replace("SQ_INSTS_", "").lower(): v / ops for k, v in inst.items()},
     "instructions_per_op": total_inst / ops,

@@ -3,6 +3,8 @@
 // Each method is the plain-loop meaning of the matching lane-parallel WaveGPU method.
 // Never linked into the product library.
 #pragma once
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -101,7 +103,16 @@ struct WaveCPU {
     for (u32 i = 0; i < (u32)L; i++) n += c[i].len != 0;
     return n;
   }
-  void cache_store(Span* p) const { for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
+  void cache_store(Span* p, u32 lo) const {
+    // entries below lo must be unchanged since the leaf was loaded (the replay's dirty tracking)
+    for (u32 i = 0; i < lo && i < (u32)L; i++) {
+      if (std::memcmp(&p[i], &c[i], sizeof(Span)) != 0) {
+        std::fprintf(stderr, "wave_cpu: cached entry %u written but below the dirty mark %u\n", i, lo);
+        std::abort();
+      }
+    }
+    for (u32 i = lo; i < (u32)L; i++) p[i] = c[i];
+  }
   Span cget(u32 i) const { return c[i & 63]; }
   u32 cget_order(u32 i) const { return c[i & 63].order; }
   i32 cget_len(u32 i) const { return c[i & 63].len; }
@@ -195,6 +206,15 @@ struct WaveCPU {
   }
   u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
     return delete_scan_b(rb, b0, nv, remote, compact, agent, delta);
+  }
+  u32 front_scan(u32 b0, u32 nv, u32 agent, u32 len) const {
+    u32 n = 1;
+    for (u32 j = b0 + 1; j < nv; j++) {
+      const Rec& r = rb[j];
+      if (!(r.w0 == ((REC_LC << 28) | agent) && r.w1 == 0u && r.w2 == 0u && r.w3 == len)) break;
+      n++;
+    }
+    return n;
   }
   static u32 typing_scan_b(const Rec* rb, u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3, u32& total) {
     if (compact) {

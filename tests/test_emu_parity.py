@@ -96,6 +96,37 @@ def test_kevin_prepends(L):
     assert diff_states(o.export(), e.export()) == []
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_front_runs_mixed(seed):
+    # runs of inserts at position 0 (replay_core.h front_run: closed form, leaf splits at index 0)
+    # of 1-3 chars, broken by deletes at the front (the next run's origin_right is then a deleted
+    # item, Q1), typing elsewhere and runs longer than the record window; tight leaf capacity so
+    # runs stop for growth and resume
+    rng = np.random.default_rng(seed)
+    counts, patches, ln = [], [], 0
+    while len(counts) < 6000:
+        k, w = int(rng.integers(1, 150)), int(rng.integers(1, 4))
+        for _ in range(k):
+            counts.append(1); patches.append((0, 0, w)); ln += w
+        r = rng.random()
+        if r < 0.4 and ln > 3:
+            d = int(rng.integers(1, 4))
+            counts.append(1); patches.append((0, d, 0)); ln -= d
+        elif r < 0.7:
+            pos = int(rng.integers(0, ln + 1))
+            for j in range(int(rng.integers(1, 6))):
+                counts.append(1); patches.append((pos + j, 0, 1)); ln += 1
+    c = np.array(counts, np.uint32)
+    p = np.array(patches, np.uint32).reshape(-1, 3)
+    for L in (32, 4):
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        assert o.apply_trace(o.agent("seph"), c, p) == 0
+        e = EmuDoc(L)
+        assert e.run_local(e.agent("seph"), c, p, 24 if L == 32 else 4) == 0
+        assert e.check() == ""
+        assert diff_states(o.export(), e.export()) == []
+
+
 @pytest.mark.parametrize("L", [32, 4])
 def test_config5_full_size(L):
     # BASELINE config 5 at its stated size: a 1M-char base, 16 agents x 64 rounds x 64 txns

@@ -358,13 +358,16 @@ def test_long_document_publish_chains():
         assert e.export(0)["canon"].shape[0] <= 2
 
 
-def test_pos_to_loc_chunks_staged_and_mixed():
-    """pos -> loc answers of the chunked kernel (k_pos_to_loc_blk: 4,096-query chunks; a chunk of one
-    document searches its visible prefix staged in LDS, any other chunk per thread in HBM) against
-    the oracle: uniform chunks, a chunk straddling two documents, interleaved documents and
-    out-of-range positions / documents in one batch."""
+@pytest.mark.parametrize("mode", ["lds", "per_thread", "merge"])
+def test_pos_to_loc_chunks_staged_and_mixed(mode):
+    """pos -> loc answers of every query kernel family against the oracle (lds: k_pos_to_loc_blk,
+    4,096-query chunks; a chunk of one document searches its visible prefix staged in LDS, any other
+    chunk per thread in HBM; merge: k_pos_to_loc_merge, a sorted chunk merges against the visible
+    prefix, others per thread): uniform chunks (sorted and unsorted), a chunk straddling two
+    documents, interleaved documents and out-of-range positions / documents in one batch."""
     names = ["sveltecomponent", "rustcode", "automerge-paper"]
     e = crdt_amd.Engine(len(names), 32)
+    e.query_kernel(mode)
     orc = []
     for d, name in enumerate(names):
         t = load_trace(name)
@@ -380,6 +383,9 @@ def test_pos_to_loc_chunks_staged_and_mixed():
     d_m = rng.integers(0, 4, 9000)  # document 3 does not exist
     docs = np.concatenate([d_u, d_m]).astype(np.uint32)
     pos = np.array([rng.integers(0, (lens[d] if d < 3 else 10) + 3) for d in docs], np.uint32)
+    pos[:8192] = np.sort(pos[:8192])       # two sorted uniform chunks (the merge path), the
+    pos[4096:8192] = np.sort(pos[4096:8192])  # second starting at its own minimum; then unsorted
+    pos[100:110] = pos[100]  # (equal positions in a sorted chunk)
     ga, gs = e.pos_to_loc(docs, pos)
     for d in range(4):
         m = docs == d

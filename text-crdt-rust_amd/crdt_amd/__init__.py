@@ -161,7 +161,9 @@ def lib():
     L.crdt_debug_state.argtypes = [vp, u32, P(u32)]
     L.crdt_fit.argtypes = [vp]
     L.crdt_set_share_streams.argtypes = [vp, C.c_int]
-    L.crdt_set_device_intern.argtypes = [vp, C.c_int]
+    for f in ("crdt_set_device_intern", "crdt_set_query_kernel"):
+        if hasattr(L, f):  # (older libraries, for A/B runs, lack them)
+            getattr(L, f).argtypes = [vp, C.c_int]
     L.crdt_apply_local_probed.argtypes = [vp, u64, P(u32), P(u64), vp, vp, vp, vp, P(i32)]
     L.crdt_mem_bytes.argtypes = [vp]
     L.crdt_mem_bytes.restype = u64
@@ -209,7 +211,7 @@ EXPORTED_SYMBOLS = [
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
     "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
-    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams", "crdt_set_device_intern",
+    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams", "crdt_set_device_intern", "crdt_set_query_kernel",
     # include/crdt_trace.h (host-only trace ingestion)
     "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
@@ -388,6 +390,13 @@ class Engine:
     def share_streams(self, on: bool = True):
         """documents staged from the same host stream read one device copy"""
         _check(self.L.crdt_set_share_streams(self.h, int(on)), "share_streams")
+
+    QUERY_KERNELS = {"lds": 0, "per_thread": 1, "merge": 2}
+
+    def query_kernel(self, mode: str):
+        """kernels behind the device query entry points: "lds" (default), "per_thread", "merge"
+        (sorted batches; same answers for any batch)"""
+        _check(self.L.crdt_set_query_kernel(self.h, self.QUERY_KERNELS[mode]), "query_kernel")
 
     def device_intern(self, on: bool = True):
         """stage_remote_replicated interns every document's authors with k_intern (same ids)"""

@@ -148,7 +148,13 @@ struct crdt_engine {
   bool has_probes = false;
   bool share_streams = false;  // documents staged with the same host stream read one device copy
   bool intern_on_device = false;  // crdt_stage_remote_replicated interns through k_intern
+  int query_kernel = -1;  // crdt_set_query_kernel (-1: not set; CRDT_QUERY_PER_THREAD selects 1)
   bool published = false;
+  int qmode() const {
+    if (query_kernel >= 0) return query_kernel;
+    static const bool per_thread = getenv("CRDT_QUERY_PER_THREAD") != nullptr;  // (A/B switch)
+    return per_thread ? CRDT_QUERY_PER_THREAD : CRDT_QUERY_LDS;
+  }
   double last_replay_ms = 0, last_publish_ms = 0, last_materialize_ms = 0;
   // text materialisation: order-indexed content streams, per-document stream offsets, output text
   u32* content = nullptr;
@@ -1442,6 +1448,12 @@ int crdt_set_share_streams(crdt_engine* e, int on) {
   return 0;
 }
 
+int crdt_set_query_kernel(crdt_engine* e, int mode) {
+  if (!e || mode < CRDT_QUERY_LDS || mode > CRDT_QUERY_MERGE) return CRDT_E_ARG;
+  e->query_kernel = mode;
+  return 0;
+}
+
 int crdt_set_device_intern(crdt_engine* e, int on) {
   if (!e) return CRDT_E_ARG;
   e->intern_on_device = on != 0;
@@ -1462,8 +1474,13 @@ int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
     if (r) return r;
   }
   if (!n) return 0;
-  static const bool per_thread = getenv("CRDT_QUERY_PER_THREAD") != nullptr;  // (A/B of the two kernels)
-  if (per_thread) {
+  int mode = e->qmode();
+  if (mode == CRDT_QUERY_MERGE) {  // sorted batches: merge path against vpos, chunk by chunk
+    u64 blocks = (n + QBLK_Q - 1) / QBLK_Q;
+    if (blocks > 0x7FFFFFFFull) return CRDT_E_ARG;
+    if (e->L == 32) hipLaunchKernelGGL(k_pos_to_loc_merge<32>, dim3((u32)blocks), dim3(QM_T), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+    else hipLaunchKernelGGL(k_pos_to_loc_merge<4>, dim3((u32)blocks), dim3(QM_T), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
+  } else if (mode == CRDT_QUERY_PER_THREAD) {
     u32 blocks = (u32)std::min<u64>((n + 255) / 256, 8192);
     if (e->L == 32) hipLaunchKernelGGL(k_pos_to_loc<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
     else hipLaunchKernelGGL(k_pos_to_loc<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, pos, agent, seq);
@@ -1485,8 +1502,10 @@ int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
   }
   if (!n) return 0;
   u32 blocks = (u32)std::min<u64>((n + 255) / 256, 8192);
-  static const bool per_thread = getenv("CRDT_QUERY_PER_THREAD") != nullptr;  // (A/B of the two kernels)
-  if (per_thread) {
+  // (merge mode: sorted (agent, seq) batches keep item_orders / bitmap / rank reads in cache, so
+  // the thread-per-query kernel needs no staging)
+  int mode = e->qmode();
+  if (mode == CRDT_QUERY_PER_THREAD || mode == CRDT_QUERY_MERGE) {
     if (e->L == 32) hipLaunchKernelGGL(k_loc_to_pos<32>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
     else hipLaunchKernelGGL(k_loc_to_pos<4>, dim3(blocks), dim3(256), 0, e->stream, e->pools_view(e->pools), e->pub_view(), (u32)e->n_docs, n, doc, agent, seq, pos, deleted);
   } else {  // chunks of QBLK_Q queries; a one-document chunk ranks orders in its LDS-staged bitmap

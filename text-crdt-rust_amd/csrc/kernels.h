@@ -1201,6 +1201,121 @@ __global__ void k_loc_to_pos(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* d
   }
 }
 
+// pos -> loc for sorted query batches by merge path (BASELINE north_star's sorted batches): a
+// chunk of QBLK_Q queries that name one document, positions ascending, is merged against the
+// document's visible prefix vpos[0..cn) (ascending, vpos[0] = 0) tile by tile.  vpos streams
+// through LDS in QM_TILE-entry tiles (coalesced, the next tile's loads in flight while the current
+// one is searched); the queries of a tile are the contiguous run of the sorted chunk below the
+// next tile's first entry, and each searches only its tile (Cursor at content pos, root.rs:54-88).
+// vpos is read once per chunk and the LDS footprint is small (24 KiB), so several chunks run per
+// CU -- unlike k_pos_to_loc_blk, which stages the whole prefix (up to 144 KiB) first.  Pass 1
+// writes each query's order into seq[], pass 2 maps orders to (agent, seq) through
+// client_with_order.  A mixed or unsorted chunk is answered per thread.
+#define QM_T 256u
+#define QM_TILE 2048u
+template <int L>
+__global__ __launch_bounds__(QM_T) void k_pos_to_loc_merge(Pools P, PubOut O, u32 n_docs, u64 nq, const u32* doc, const u32* pos,
+                                                          u16* agent, u32* seq) {
+  __shared__ u32 s_q[QBLK_Q];
+  __shared__ u32 s_a[QM_TILE];
+  __shared__ u32 s_bad;
+  const u32 t = threadIdx.x;
+  const u64 q0 = (u64)blockIdx.x * QBLK_Q;
+  const u64 q1 = q0 + QBLK_Q < nq ? q0 + QBLK_Q : nq;
+  const u32 nb = (u32)(q1 - q0);
+  const u32 d0 = doc[q0];
+  if (t == 0) s_bad = 0;
+  for (u32 j = t; j < nb; j += QM_T) s_q[j] = pos[q0 + j];
+  __syncthreads();
+  u32 bad = 0;
+  for (u32 j = t; j < nb; j += QM_T) {  // one document, positions ascending
+    bad |= doc[q0 + j] != d0 ? 1u : 0u;
+    if (j) bad |= s_q[j - 1] > s_q[j] ? 1u : 0u;
+  }
+  if (bad) s_bad = 1;  // (any writer stores the same value)
+  __syncthreads();
+  i32 stt = d0 < n_docs ? P.st[d0].status : ST_BAD_INPUT;
+  if (s_bad || d0 >= n_docs || !(stt == ST_OK || stt == ST_NEED_CAPACITY)) {
+    for (u64 q = q0 + t; q < q1; q += QM_T) {
+      u32 d = doc[q], p = pos[q];
+      u16 a = 0xFFFF;
+      u32 sq = INVALID;
+      if (d < n_docs) {
+        i32 s2 = P.st[d].status;
+        if ((s2 == ST_OK || s2 == ST_NEED_CAPACITY) && p < O.len[d]) {
+          DocSeg sg = P.seg[d];
+          const u32* vp = O.vpos + sg.canon_base;
+          u32 lo = 0, hi = O.canon_n[d];
+          while (lo < hi) {
+            u32 mid = (lo + hi) >> 1;
+            if (vp[mid] <= p) lo = mid + 1; else hi = mid;
+          }
+          u32 k = lo - 1;
+          u32 order = O.corder[sg.canon_base + k] + (p - vp[k]);
+          const CwoRun* cw = P.cwo + sg.cwo_base;
+          i32 r = find_run(cw, P.st[d].n_cwo, order);
+          if (r >= 0) { a = (u16)cw[r].agent; sq = cw[r].seq + (order - cw[r].key); }
+        }
+      }
+      agent[q] = a;
+      seq[q] = sq;
+    }
+    return;
+  }
+  const DocSeg sg = P.seg[d0];
+  const u32 cn = O.canon_n[d0], dlen = O.len[d0];
+  const u32* A = O.vpos + sg.canon_base;
+  const u32* co = O.corder + sg.canon_base;
+  constexpr u32 PT = QM_TILE / QM_T;  // tile entries per thread
+  u32 nx[PT];
+#pragma unroll
+  for (u32 u = 0; u < PT; u++) nx[u] = u * QM_T + t < cn ? A[u * QM_T + t] : 0u;
+  u32 qa = 0;  // queries [0, qa) answered
+  for (u32 ts = 0; ts < cn && qa < nb; ts += QM_TILE) {
+    const u32 tn = cn - ts < QM_TILE ? cn - ts : QM_TILE;
+#pragma unroll
+    for (u32 u = 0; u < PT; u++) s_a[u * QM_T + t] = nx[u];
+    const u32 te = ts + QM_TILE;
+    const u32 bound = te < cn ? A[te] : INVALID;  // the next tile's first entry (queries below it are here)
+#pragma unroll
+    for (u32 u = 0; u < PT; u++) nx[u] = te + u * QM_T + t < cn ? A[te + u * QM_T + t] : 0u;  // next tile, in flight
+    __syncthreads();
+    // this tile's queries: [qa, qb), qb = the first query >= bound (every thread alike)
+    u32 lo = qa, hi = nb;
+    while (lo < hi) {
+      u32 mid = (lo + hi) >> 1;
+      if (s_q[mid] < bound) lo = mid + 1; else hi = mid;
+    }
+    const u32 qb = bound == INVALID ? nb : lo;
+    for (u32 j = qa + t; j < qb; j += QM_T) {
+      u32 p = s_q[j];
+      u32 l2 = 0, h2 = tn;  // the last tile entry <= p (s_a[0] <= p: earlier queries are answered)
+      while (l2 < h2) {
+        u32 mid = (l2 + h2) >> 1;
+        if (s_a[mid] <= p) l2 = mid + 1; else h2 = mid;
+      }
+      u32 k = l2 - 1u;
+      seq[q0 + j] = p < dlen ? co[ts + k] + (p - s_a[k]) : INVALID;
+    }
+    qa = qb;
+    __syncthreads();
+  }
+  // pass 2: order -> (agent, seq), client_with_order.get (simple_rle.rs:98-103)
+  const CwoRun* cw = P.cwo + sg.cwo_base;
+  const u32 ncwo = P.st[d0].n_cwo;
+  for (u64 q = q0 + t; q < q1; q += QM_T) {
+    u32 order = (u32)(q - q0) < qa ? seq[q] : INVALID;  // (an empty document answers nothing)
+    u16 a = 0xFFFF;
+    u32 sq = INVALID;
+    if (order != INVALID) {
+      i32 r = find_run(cw, ncwo, order);
+      if (r >= 0) { a = (u16)cw[r].agent; sq = cw[r].seq + (order - cw[r].key); }
+    }
+    agent[q] = a;
+    seq[q] = sq;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Agent-name interning on the device (ListCRDT::get_or_create_agent_id, doc.rs:66-89; SURVEY
 // §8f row 3).  One wave per group (a document's name references in call order): ids in order of

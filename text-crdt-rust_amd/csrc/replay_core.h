@@ -189,7 +189,7 @@ struct Replayer {
     p(C_BLK, 0);
     p(C_I, 0);
     p(C_VSTART, 0);
-    p(C_DIRTY, 0);
+    p(C_DIRTY, (u32)L);
     p(C_VS_OK, 0);
     p(C_SUCC, INVALID);
     p(C_SUCC_ORD, 0);
@@ -361,13 +361,20 @@ struct Replayer {
   }
 
   // ------------------------------------------------------------------ leaf cache
+  // The cached leaf's lowest written entry (C_DIRTY; L = clean): a commit writes back entries
+  // [lo, L) only, since the ones below it still equal the leaf in HBM.
+  CRDT_HD void dirty(u32 i) {
+    u32 lo = g(C_DIRTY);
+    p(C_DIRTY, i < lo ? i : lo);
+  }
   CRDT_HD void commit() {
     u32 lf = g(C_LEAF);
     if (lf == INVALID) return;
-    if (!g(C_DIRTY)) return;
-    w.cache_store(leafp(lf));
+    u32 lo = g(C_DIRTY);
+    if (lo >= (u32)L) return;
+    w.cache_store(leafp(lf), lo);  // (entries below the lowest written one are unchanged)
     dir_set_cached_vis(g(C_NOW));
-    p(C_DIRTY, 0);
+    p(C_DIRTY, (u32)L);
   }
   // Cache `leaf`; `slot` = its directory slot (blk << 6 | i), possibly a load still in flight:
   // the leaf's entries are requested before the slot is first used, so both arrive together.
@@ -378,7 +385,7 @@ struct Replayer {
     p(C_LEAF, leaf);
     p(C_BLK, sl >> 6);
     p(C_I, sl & 63u);
-    p(C_DIRTY, 0);
+    p(C_DIRTY, (u32)L);
     u32 v = w.cache_vis_from(0u);
     p(C_NOW, v);
     p(C_VIS, v);
@@ -405,7 +412,7 @@ struct Replayer {
   CRDT_HD void set(u32 idx, const Span& e) {
     p(C_NOW, g(C_NOW) - clen_i(w.cget_len(idx)) + clen(e));
     w.cset(idx, e);
-    p(C_DIRTY, 1);
+    dirty(idx);
   }
   CRDT_HD static u32 clen_i(i32 len) { return len > 0 ? (u32)len : 0u; }
   CRDT_HD static u32 slen_i(i32 len) { return (u32)(len < 0 ? -len : len); }
@@ -558,7 +565,7 @@ struct Replayer {
     w.cache_clear(idx, n);
     p(C_NOW, g(C_NOW) - stolen);
     p(C_N, idx);
-    p(C_DIRTY, 1);
+    dirty(idx);
     // link nl right after the cached leaf (directory block insert; the block splits when full)
     u32 blk = g(C_BLK), i = g(C_I);
     u32 ng = g(S_NG);
@@ -657,7 +664,7 @@ struct Replayer {
         w.cache_from_moved();
         u32 v = w.cache_vis_from(0u);
         p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
-        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 0); p(C_VS_OK, 0);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, (u32)L); p(C_VS_OK, 0);
         p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
         p(C_N, space + moved);
         c.leaf = nl;
@@ -1374,7 +1381,7 @@ struct Replayer {
     e.len += (i32)total;
     w.cset(idx, e);  // (e is visible: the count grows by total)
     p(C_NOW, g(C_NOW) + total);
-    p(C_DIRTY, 1u);
+    dirty(idx);
     inc(S_N_ITEMS, total);
     fast_txn_commit(first, total);
     return nt * per_txn(remote);
@@ -1418,7 +1425,7 @@ struct Replayer {
       inc(S_N_ENTRIES, m);
     }
     p(C_NOW, g(C_NOW) - l);
-    p(C_DIRTY, 1u);
+    dirty(idx);
     return 1;
   }
   // A run of k >= 2 one-item deletes in closed form (the per-op rules of leaf_delete, solved once):
@@ -1495,7 +1502,7 @@ struct Replayer {
     p(C_N, n + delta);
     inc(S_N_ENTRIES, delta);
     p(C_NOW, g(C_NOW) - k);
-    p(C_DIRTY, 1u);
+    dirty(idx);
     return k;
   }
   // Delete txns: the one at b0 (l items at `off` of entry idx) and, when it deletes one item, the
@@ -1687,7 +1694,7 @@ struct Replayer {
     // visible pieces still to place are off its count
     u32 unplaced_vis = (hc && !pre) ? (u32)pc.len : 0u;
     p(C_NOW, g(C_NOW) - l - unplaced_vis);
-    p(C_DIRTY, 1u);
+    dirty(idx);
     (void)pre_vis;
     if (m == 0u) return;
     inc(S_N_ENTRIES, m);
@@ -1717,7 +1724,7 @@ struct Replayer {
         w.cache_from_moved();
         u32 v = w.cache_vis_from(0u);
         p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
-        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 1u); p(C_VS_OK, 0);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 0u); p(C_VS_OK, 0);
         p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
         p(C_N, m + moved);
         leaf = nl;
@@ -1742,8 +1749,9 @@ struct Replayer {
   // the entry at the cursor (remainder after the item) and makes room, without a leaf split.
   // Returns 0, having changed nothing, when the leaf or the order map has no room.
   // front: the cursor is at offset 0 of entry 0 (a local insert at position 0; never remote)
-  CRDT_HD u32 leaf_insert(u32 idx, u32 off, const Span& item, u32 front) {
-    if (front) return leaf_insert_front(item);
+  // (kf: the length of the front run this txn starts, see leaf_insert_front; returns txns placed)
+  CRDT_HD u32 leaf_insert(u32 idx, u32 off, const Span& item, u32 front, u32 kf) {
+    if (front) return leaf_insert_front(item, kf);
     Span e = w.cget(idx);
     u32 n = g(C_N);
     u32 len = (u32)item.len;
@@ -1766,26 +1774,41 @@ struct Replayer {
     map_fill(item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
     w.cset(idx + 1u, item);
     p(C_NOW, g(C_NOW) + len);
-    p(C_DIRTY, 1u);
+    dirty(idx);
     inc(S_N_ITEMS, len);
     return 1;
   }
   // The item as entry 0 of the cached first leaf (cursor at the start of the document, offset 0 at
-  // index 0: insert_internal neither rolls back nor splits, mutations.rs:34-52) without a leaf split.
-  CRDT_HD u32 leaf_insert_front(const Span& item) {
+  // index 0: insert_internal neither rolls back nor splits, mutations.rs:34-52) without a leaf split
+  // -- and with it the rest of a front run: k local txns that each insert len chars at position 0
+  // (the reference's `kevin` benchmark shape, benches/yjs.rs:51-62).  Prepend j (0-based) gets
+  // orders first + j*len, origin_left ROOT and origin_right = the item at position 0 before it
+  // (the item's for j = 0, else prepend j-1's first item; doc.rs:443-453); integrate stops at once
+  // and insert_internal puts it at index 0, never prepending it onto entry 0 (orders only grow).
+  // So the prepends that fit the leaf are one shift plus one lane-parallel write, newest at lane
+  // 0; the one that finds the leaf full goes the general way (a split at index 0).  Returns the
+  // txns placed (0: no room, nothing changed).
+  CRDT_HD u32 leaf_insert_front(const Span& item, u32 k) {
     u32 n = g(C_N);
     u32 len = (u32)item.len;
-    if (n + 1u > (u32)L) return 0;
-    if (g(K_MAP) - item.order < len) return 0;
-    w.cache_shift_right(0u, n, 1u);
-    p(C_N, n + 1u);
-    inc(S_N_ENTRIES, 1u);
-    map_fill(item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
-    w.cset(0u, item);
-    p(C_NOW, g(C_NOW) + len);
-    p(C_DIRTY, 1u);
-    inc(S_N_ITEMS, len);
-    return 1;
+    u32 m = (u32)L - n;
+    m = m < k ? m : k;
+    if (m == 0u) return 0;
+    if (g(K_MAP) - item.order < m * len) return 0;
+    w.cache_shift_right(0u, n, m);
+    p(C_N, n + m);
+    inc(S_N_ENTRIES, m);
+    map_fill(item.order, m * len, g(C_LEAF));  // notify (doc.rs:143-153)
+    u32 top = m - 1u, first = item.order, orr0 = item.orr;
+    w.cset_lanes(0u, m, [&](u32 lane) {
+      u32 j = top - lane;
+      u32 o = first + j * len;
+      return Span{o, ROOT_ORDER, j == 0u ? orr0 : o - len, (i32)len};
+    });
+    p(C_NOW, g(C_NOW) + m * len);
+    p(C_DIRTY, 0u);
+    inc(S_N_ITEMS, m * len);
+    return m;
   }
   // A local delete of l visible items that starts at offset `off` of visible entry idx of the
   // cached leaf and runs past that entry (rem: the visible position of its first item within the
@@ -1882,7 +1905,7 @@ struct Replayer {
     p(C_N, n);
     inc(S_N_ENTRIES, add);
     p(C_NOW, g(C_NOW) - l);
-    p(C_DIRTY, 1u);
+    dirty(idx);
     fast_txn_commit(first, l);
     return 1;
   }
@@ -2037,9 +2060,14 @@ struct Replayer {
       u32 total;
       u32 nt = typing_run(b0, nv, remote, agent, (agent & 0xFFFFu) | (o.w1 & 0xFFFF0000u), o, total);
       item.len = (i32)total;
-      if (!leaf_insert(idx, c.off, item, remote ? 0u : (c.off == 0u ? 1u : 0u))) return 0;
+      // a local insert at position 0 (offset 0 only there) may start a front run
+      u32 front = remote ? 0u : (c.off == 0u ? 1u : 0u);
+      u32 kf = (front & cpt) && nt == 1u ? w.front_scan(b0, nv, agent, l) : 1u;
+      u32 r = leaf_insert(idx, c.off, item, front, kf);
+      if (!r) return 0;
+      total += (r - 1u) * l;  // (r > 1 only for a front run, whose first txn is the item: total == l)
       fast_txn_commit(first, total);
-      return nt * per;
+      return (nt + r - 1u) * per;
     }
     i32 el = w.cget_len(idx);
     if (el <= 0) return 0;                // already deleted

@@ -318,9 +318,9 @@ struct WaveGPU {
     eo = in ? v.x : 0u; el = in ? v.y : 0u; er = in ? v.z : 0u; en = in ? (i32)v.w : 0;
     return __popcll(ballot(en != 0));
   }
-  __device__ __forceinline__ void cache_store(Span* p) const {
+  __device__ __forceinline__ void cache_store(Span* p, u32 lo) const {  // entries [lo, L)
     u32 l = lane();
-    if (l < (u32)L) *(uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
+    if (l - lo < (u32)L - lo) *(uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
   }
   __device__ __forceinline__ Span cget(u32 i) const {
     return Span{rdlane(eo, i), rdlane(el, i), rdlane(er, i), (i32)rdlane((u32)en, i)};
@@ -622,6 +622,16 @@ struct WaveGPU {
     u64 stop = ballot(l >= b0 + per && (!ok || l >= nv));
     u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
     return remote ? ((f - b0) * 43u) >> 7 : (f - b0) >> 1;
+  }
+  // Front-run scan (replay_core.h front_run): lane k checks compact local record k against "one
+  // LocalOp inserting `len` chars at position 0 by `agent`" (the txn at b0 was checked by the
+  // caller).  Returns the run length in txns (>= 1).
+  __device__ __forceinline__ u32 front_scan(u32 b0, u32 nv, u32 agent, u32 len) const {
+    u32 l = lane();
+    u32 d = (rx ^ ((REC_LC << 28) | agent)) | ry | rz | (rw ^ len);
+    u64 stop = ballot(d != 0u || l >= nv) & (~1ull << b0);
+    u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
+    return f - b0;
   }
   // The scans over the record window, and over the 64 records at p (loaded here, waited for; the
   // window does not move: only Replayer::rec moves it).  len0: the length of the txn at p.
