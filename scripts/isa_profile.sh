@@ -24,9 +24,13 @@ import sys; sys.path.insert(0, '$ROOT/text-crdt-rust_amd')
 from emu_lib import EmuDoc
 from crdt_amd.traces import load_remote_wire, load_trace
 e = EmuDoc(32)
-assert e.run_wire(load_remote_wire('$TRACE'), 64) == 0
-t = load_trace('$TRACE')
-print(int(t.patches.shape[0]) if t.patches.ndim > 1 else len(t.patches) // 3)
+if '$TRACE' == 'config4':  # generated ops (bench_config4.py's shape, one document)
+    assert e.run_random(e.agent('gen'), 20000, 0xC0FFEE, 64) == 0
+    print(20000)
+else:
+    assert e.run_wire(load_remote_wire('$TRACE'), 64) == 0
+    t = load_trace('$TRACE')
+    print(int(t.patches.shape[0]) if t.patches.ndim > 1 else len(t.patches) // 3)
 ")
 ( cd $OUT/cov && gcov -o . $ROOT/tests/emu/emu.cpp > /dev/null 2>&1 || true )
 python $ROOT/scripts/isa_dynamic.py $OUT/dev.o $OUT/dis.txt $OUT/dwarf.txt $OUT/lines.txt $OUT/cov $OPS $TOP

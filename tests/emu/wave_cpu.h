@@ -103,16 +103,7 @@ struct WaveCPU {
     for (u32 i = 0; i < (u32)L; i++) n += c[i].len != 0;
     return n;
   }
-  void cache_store(Span* p, u32 lo) const {
-    // entries below lo must be unchanged since the leaf was loaded (the replay's dirty tracking)
-    for (u32 i = 0; i < lo && i < (u32)L; i++) {
-      if (std::memcmp(&p[i], &c[i], sizeof(Span)) != 0) {
-        std::fprintf(stderr, "wave_cpu: cached entry %u written but below the dirty mark %u\n", i, lo);
-        std::abort();
-      }
-    }
-    for (u32 i = lo; i < (u32)L; i++) p[i] = c[i];
-  }
+  void cache_store(Span* p) const { for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
   Span cget(u32 i) const { return c[i & 63]; }
   u32 cget_order(u32 i) const { return c[i & 63].order; }
   i32 cget_len(u32 i) const { return c[i & 63].len; }

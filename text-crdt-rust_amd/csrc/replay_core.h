@@ -189,7 +189,7 @@ struct Replayer {
     p(C_BLK, 0);
     p(C_I, 0);
     p(C_VSTART, 0);
-    p(C_DIRTY, (u32)L);
+    p(C_DIRTY, 0);
     p(C_VS_OK, 0);
     p(C_SUCC, INVALID);
     p(C_SUCC_ORD, 0);
@@ -361,20 +361,13 @@ struct Replayer {
   }
 
   // ------------------------------------------------------------------ leaf cache
-  // The cached leaf's lowest written entry (C_DIRTY; L = clean): a commit writes back entries
-  // [lo, L) only, since the ones below it still equal the leaf in HBM.
-  CRDT_HD void dirty(u32 i) {
-    u32 lo = g(C_DIRTY);
-    p(C_DIRTY, i < lo ? i : lo);
-  }
   CRDT_HD void commit() {
     u32 lf = g(C_LEAF);
     if (lf == INVALID) return;
-    u32 lo = g(C_DIRTY);
-    if (lo >= (u32)L) return;
-    w.cache_store(leafp(lf), lo);  // (entries below the lowest written one are unchanged)
+    if (!g(C_DIRTY)) return;
+    w.cache_store(leafp(lf));
     dir_set_cached_vis(g(C_NOW));
-    p(C_DIRTY, (u32)L);
+    p(C_DIRTY, 0);
   }
   // Cache `leaf`; `slot` = its directory slot (blk << 6 | i), possibly a load still in flight:
   // the leaf's entries are requested before the slot is first used, so both arrive together.
@@ -385,7 +378,7 @@ struct Replayer {
     p(C_LEAF, leaf);
     p(C_BLK, sl >> 6);
     p(C_I, sl & 63u);
-    p(C_DIRTY, (u32)L);
+    p(C_DIRTY, 0);
     u32 v = w.cache_vis_from(0u);
     p(C_NOW, v);
     p(C_VIS, v);
@@ -412,7 +405,7 @@ struct Replayer {
   CRDT_HD void set(u32 idx, const Span& e) {
     p(C_NOW, g(C_NOW) - clen_i(w.cget_len(idx)) + clen(e));
     w.cset(idx, e);
-    dirty(idx);
+    p(C_DIRTY, 1u);
   }
   CRDT_HD static u32 clen_i(i32 len) { return len > 0 ? (u32)len : 0u; }
   CRDT_HD static u32 slen_i(i32 len) { return (u32)(len < 0 ? -len : len); }
@@ -565,7 +558,7 @@ struct Replayer {
     w.cache_clear(idx, n);
     p(C_NOW, g(C_NOW) - stolen);
     p(C_N, idx);
-    dirty(idx);
+    p(C_DIRTY, 1u);
     // link nl right after the cached leaf (directory block insert; the block splits when full)
     u32 blk = g(C_BLK), i = g(C_I);
     u32 ng = g(S_NG);
@@ -664,7 +657,7 @@ struct Replayer {
         w.cache_from_moved();
         u32 v = w.cache_vis_from(0u);
         p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
-        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, (u32)L); p(C_VS_OK, 0);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 0); p(C_VS_OK, 0);
         p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
         p(C_N, space + moved);
         c.leaf = nl;
@@ -1381,7 +1374,7 @@ struct Replayer {
     e.len += (i32)total;
     w.cset(idx, e);  // (e is visible: the count grows by total)
     p(C_NOW, g(C_NOW) + total);
-    dirty(idx);
+    p(C_DIRTY, 1u);
     inc(S_N_ITEMS, total);
     fast_txn_commit(first, total);
     return nt * per_txn(remote);
@@ -1425,7 +1418,7 @@ struct Replayer {
       inc(S_N_ENTRIES, m);
     }
     p(C_NOW, g(C_NOW) - l);
-    dirty(idx);
+    p(C_DIRTY, 1u);
     return 1;
   }
   // A run of k >= 2 one-item deletes in closed form (the per-op rules of leaf_delete, solved once):
@@ -1502,7 +1495,7 @@ struct Replayer {
     p(C_N, n + delta);
     inc(S_N_ENTRIES, delta);
     p(C_NOW, g(C_NOW) - k);
-    dirty(idx);
+    p(C_DIRTY, 1u);
     return k;
   }
   // Delete txns: the one at b0 (l items at `off` of entry idx) and, when it deletes one item, the
@@ -1694,7 +1687,7 @@ struct Replayer {
     // visible pieces still to place are off its count
     u32 unplaced_vis = (hc && !pre) ? (u32)pc.len : 0u;
     p(C_NOW, g(C_NOW) - l - unplaced_vis);
-    dirty(idx);
+    p(C_DIRTY, 1u);
     (void)pre_vis;
     if (m == 0u) return;
     inc(S_N_ENTRIES, m);
@@ -1724,7 +1717,7 @@ struct Replayer {
         w.cache_from_moved();
         u32 v = w.cache_vis_from(0u);
         p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
-        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 0u); p(C_VS_OK, 0);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 1u); p(C_VS_OK, 0);
         p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
         p(C_N, m + moved);
         leaf = nl;
@@ -1774,7 +1767,7 @@ struct Replayer {
     map_fill(item.order, len, g(C_LEAF));  // notify (doc.rs:143-153)
     w.cset(idx + 1u, item);
     p(C_NOW, g(C_NOW) + len);
-    dirty(idx);
+    p(C_DIRTY, 1u);
     inc(S_N_ITEMS, len);
     return 1;
   }
@@ -1806,7 +1799,7 @@ struct Replayer {
       return Span{o, ROOT_ORDER, j == 0u ? orr0 : o - len, (i32)len};
     });
     p(C_NOW, g(C_NOW) + m * len);
-    p(C_DIRTY, 0u);
+    p(C_DIRTY, 1u);
     inc(S_N_ITEMS, m * len);
     return m;
   }
@@ -1905,7 +1898,7 @@ struct Replayer {
     p(C_N, n);
     inc(S_N_ENTRIES, add);
     p(C_NOW, g(C_NOW) - l);
-    dirty(idx);
+    p(C_DIRTY, 1u);
     fast_txn_commit(first, l);
     return 1;
   }

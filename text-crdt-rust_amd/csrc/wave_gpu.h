@@ -318,9 +318,9 @@ struct WaveGPU {
     eo = in ? v.x : 0u; el = in ? v.y : 0u; er = in ? v.z : 0u; en = in ? (i32)v.w : 0;
     return __popcll(ballot(en != 0));
   }
-  __device__ __forceinline__ void cache_store(Span* p, u32 lo) const {  // entries [lo, L)
+  __device__ __forceinline__ void cache_store(Span* p) const {
     u32 l = lane();
-    if (l - lo < (u32)L - lo) *(uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
+    if (l < (u32)L) *(uint4*)(p + l) = make_uint4(eo, el, er, (u32)en);
   }
   __device__ __forceinline__ Span cget(u32 i) const {
     return Span{rdlane(eo, i), rdlane(el, i), rdlane(er, i), (i32)rdlane((u32)en, i)};
@@ -623,7 +623,7 @@ struct WaveGPU {
     u32 f = stop ? (u32)__builtin_ctzll(stop) : 64u;
     return remote ? ((f - b0) * 43u) >> 7 : (f - b0) >> 1;
   }
-  // Front-run scan (replay_core.h front_run): lane k checks compact local record k against "one
+  // Front-run scan (replay_core.h leaf_insert_front): lane k checks compact local record k against "one
   // LocalOp inserting `len` chars at position 0 by `agent`" (the txn at b0 was checked by the
   // caller).  Returns the run length in txns (>= 1).
   __device__ __forceinline__ u32 front_scan(u32 b0, u32 nv, u32 agent, u32 len) const {
