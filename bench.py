@@ -273,6 +273,71 @@ def materialize_leg(eng, trace, n, hip, ev, s_, reps=5):
             "parity": "every document's text digest == committed golden text digest (== endContent FNV, tests/golden)"}
 
 
+def stated_size_leg(args, wire, n_ops_doc, hip, docs=4096, steps=3):
+    """BASELINE config 2 at its stated size (4,096 documents per GPU; the bench line runs 8,192 = 8
+    waves per SIMD): the same step (reset + replay + publish + the same per-document queries) on a
+    second engine, timed the same way.  Reported beside the line, not as its value."""
+    import ctypes as C
+    import crdt_amd
+    import torch
+    e = crdt_amd.Engine(docs, 32)
+    e.device_intern(not args.host_intern)
+    e.stage_remote_replicated(wire, 0, [doc_name(i) for i in range(docs)])
+    assert (e.run() == 0).all()
+    e.publish_async()
+    e.sync()
+    e.fit()
+    q = args.queries
+    lens = e.lens()
+    rng = np.random.default_rng(4321)
+    dev = torch.device("cuda", 0)
+    d_doc = torch.from_numpy(np.repeat(np.arange(docs, dtype=np.uint32), q).view(np.int32)).to(dev)
+    d_pos = torch.from_numpy((rng.random(docs * q) * np.repeat(lens, q)).astype(np.uint32).view(np.int32)).to(dev)
+    d_ag = torch.zeros(docs * q, dtype=torch.int16, device=dev)
+    d_seq = torch.zeros(docs * q, dtype=torch.int32, device=dev)
+    d_p2 = torch.zeros(docs * q, dtype=torch.int32, device=dev)
+    d_del = torch.zeros(docs * q, dtype=torch.uint8, device=dev)
+    ev = [C.c_void_p() for _ in range(2)]
+    for x in ev:
+        hip.hipEventCreate(C.byref(x))
+    s_ = C.c_void_p(e.stream())
+    L = e.L
+
+    def step(ms):
+        e.reset_async()
+        hip.hipEventRecord(ev[0], s_)
+        e.run_async()
+        hip.hipEventRecord(ev[1], s_)
+        e.publish_async()
+        if q:
+            L.crdt_pos_to_loc_dev_async(e.h, docs * q, d_doc.data_ptr(), d_pos.data_ptr(), d_ag.data_ptr(), d_seq.data_ptr())
+            L.crdt_loc_to_pos_dev_async(e.h, docs * q, d_doc.data_ptr(), d_ag.data_ptr(), d_seq.data_ptr(),
+                                        d_p2.data_ptr(), d_del.data_ptr())
+        if ms is not None:
+            hip.hipEventSynchronize(ev[1])
+            x = C.c_float()
+            hip.hipEventElapsedTime(C.byref(x), ev[0], ev[1])
+            ms.append(x.value)
+
+    step(None)
+    e.sync()
+    torch.cuda.synchronize()
+    ms = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(ms)
+    e.sync()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    gold = golden(args.trace, "remote_digest")
+    ok = bool((e.status() == 0).all()) and (gold is None or bool((e.digests() == np.uint64(int(gold, 16))).all()))
+    ok = ok and (not q or bool(((d_p2 == d_pos) & (d_del == 0)).all().item()))
+    e.close()
+    return {"docs_per_gpu": docs, "waves_per_simd": docs / SIMDS, "steps": steps, "ms_per_step": el / steps * 1e3,
+            "value": docs * n_ops_doc * steps / el, "k_replay_ms": float(np.mean(ms)), "parity_ok": ok,
+            "note": "BASELINE config 2's stated size; same step and timing as the line"}
+
+
 def rehearse_cpu(args, world, rank, dist):
     """--rehearse-cpu: launch, shard and collectives exactly as on the GPU path, on CPU ranks over
     gloo; each document's 'result' is the committed golden digest (no engine, no GPU)."""
@@ -305,6 +370,7 @@ def main():
                     help="intern the per-document client names on the host (default: k_intern on the GPU)")
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
     ap.add_argument("--rehearse-cpu", action="store_true", help="CPU/gloo rehearsal of the multi-rank plumbing")
+    ap.add_argument("--no-stated-size", action="store_true", help="skip the 4,096-document (BASELINE size) leg")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the multi-rank path on one GPU: every rank runs its engine on cuda:0 and "
                          "the collectives go over gloo (CPU tensors); not a scaling measurement")
@@ -424,6 +490,9 @@ def main():
     gold = int(gold, 16) if gold else None
     ok = ok and q_ok and bool((all_dg == all_dg[0]).all()) and (gold is None or int(all_dg[0]) == gold)
     mat = materialize_leg(eng, args.trace, n, hip, ev, s_) if not args.no_text else None
+    stated = None
+    if world == 1 and n != 4096 and not args.no_stated_size:
+        stated = stated_size_leg(args, wire, n_ops_doc, hip)
     total_ops = n_ops_doc * int(all_dg.shape[0]) * args.steps
     value = total_ops / t_max
     ms_step = t_max / args.steps * 1e3
@@ -474,6 +543,7 @@ def main():
             "stage_s": stage_s,
             "stage_intern": "host" if args.host_intern else "device (k_intern)",
             "materialize": mat,
+            "stated_size": stated,
         }
         print(json.dumps(out))
     if dist is not None:

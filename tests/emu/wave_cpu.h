@@ -337,7 +337,15 @@ struct WaveCPU {
     }
     return false;
   }
-  void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+  // (the GPU's row_ld returns a row one slot per lane; here a digest of the row, which blk_insert
+  // checks against the row's current contents: the early-requested rows must still be current)
+  static u32 row_digest(const u32* p) { u32 h = 2166136261u; for (u32 k = 0; k < 64; k++) h = (h ^ p[k]) * 16777619u; return h; }
+  u32 row_ld(const u32* p) const { return row_digest(p); }
+  void blk_insert(u32 ol, u32 ov, u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+    if (ol != row_digest(dl) || ov != row_digest(dv)) {
+      std::fprintf(stderr, "wave_cpu: directory row changed between row_ld and blk_insert\n");
+      std::abort();
+    }
     for (u32 k = cnt; k > i; k--) { dl[k] = dl[k - 1]; dv[k] = dv[k - 1]; }
     dl[i] = leaf;
     dv[i] = vis;

@@ -35,7 +35,10 @@ constexpr u32 GROUP = 64;                 // directory slots per block (one wave
 // CU's LDS, so a document can have up to ROOT_CAP_MAX blocks = at least 32*(ROOT_CAP_MAX-1)
 // leaves (every block but the first holds >= 32 slots) = 13.9M entries at the release layout.
 constexpr u32 ROOT_CAP_MIN = 256;
-constexpr u32 ROOT_CAP_MAX = 13632;       // floor(163840 / 12 / 64) * 64
+constexpr u32 ROOT_CAP_MAX = 13632;       // floor(163840 / 12 / 64) * 64 (two-level root's top entries)
+// The flat LDS root also keeps a block -> group map (4 B per group: 16 B per group in all), so its
+// largest class is floor(163840 / 16 / 64) * 64 groups; documents past it use the two-level root.
+constexpr u32 ROOT_CAP_LDS = 10240;
 // Past it the root has two levels (wave_gpu.h HR): LDS top entries of rows that hold 32..64 groups
 // each in HBM, up to ROOT_CAP_MAX - 64 top entries (LDS: 12 B each + two words) -- over 434k
 // groups, 13.9M leaves, 445M entries at the release layout.

@@ -93,15 +93,16 @@ inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
 
 // Launch shape of a wave-per-document kernel whose waves hold an LDS root of `rcap` groups:
 // up to 4 waves per workgroup within the 160 KiB a workgroup may declare.
-// (hr: the two-level root: rcap top entries + two words per wave)
+// (flat root: blk / cnt / vis + the block -> group map, 16 B per group; hr: the two-level root:
+// rcap top entries of 12 B + two words per wave)
 struct LaunchShape { u32 wpb, rcap; size_t lds; };
 inline LaunchShape launch_shape(u32 rcap, bool hr = false) {
-  u32 per_wave = 12u * rcap + (hr ? 8u : 0u);
+  u32 per_wave = hr ? 12u * rcap + 8u : 16u * rcap;
   u32 wpb = std::max<u32>(1u, std::min<u32>(WAVES_PER_BLOCK, 163840u / per_wave));
   return LaunchShape{wpb, rcap, (size_t)wpb * per_wave};
 }
 // LDS root classes: a launch serves documents whose root fits its class.
-constexpr u32 ROOT_CLASSES[4] = {ROOT_CAP_MIN, 1024, 4096, ROOT_CAP_MAX};
+constexpr u32 ROOT_CLASSES[4] = {ROOT_CAP_MIN, 1024, 4096, ROOT_CAP_LDS};
 inline u32 root_class(u32 grp_cap) {
   for (u32 c : ROOT_CLASSES) if (grp_cap <= c) return c;
   return 0;  // past the LDS root: the two-level root (hroot_top)

@@ -58,7 +58,7 @@ __device__ __forceinline__ WaveGPU<L, HR> wave_with_root(u32 rcap) {
   // the LDS address space survives into the member: root accesses are ds_* (lgkmcnt only);
   // a generic pointer would make them flat ops, whose waits also drain every pending store
   w.rcap = rcap;
-  w.rt = (typename WaveGPU<L, HR>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * (3u * rcap + (HR ? 2u : 0u)));
+  w.rt = (typename WaveGPU<L, HR>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * (HR ? 3u * rcap + 2u : 4u * rcap));
   return w;
 }
 // Document of the calling wave: wave k of the launch takes list[k] (or k without a list).

@@ -671,6 +671,7 @@ struct WaveGPU {
   __device__ __forceinline__ lds_u32* rblk() const { return rt; }
   __device__ __forceinline__ lds_u32* rcnt() const { return rt + rcap; }
   __device__ __forceinline__ lds_u32* rvis() const { return rt + 2 * rcap; }
+  __device__ __forceinline__ lds_u32* gob() const { return rt + 3 * rcap; }  // block -> group (!HR)
   __device__ __forceinline__ lds_u32* trow() const { return rt; }
   __device__ __forceinline__ lds_u32* tcnt() const { return rt + rcap; }
   __device__ __forceinline__ lds_u32* tvis() const { return rt + 2 * rcap; }
@@ -770,6 +771,7 @@ struct WaveGPU {
       rblk()[0] = blk;  // every lane stores the same value: no branch
       rcnt()[0] = cnt;
       rvis()[0] = vis;
+      gob()[blk] = 0u;
     }
   }
   __device__ __forceinline__ void root_load(const GroupRec* g, u32 ng) {
@@ -802,6 +804,7 @@ struct WaveGPU {
         rblk()[i] = x.x;
         rcnt()[i] = x.y;
         rvis()[i] = x.z;
+        gob()[x.x] = i;
       }
     }
   }
@@ -852,14 +855,8 @@ struct WaveGPU {
       u32 t = hr_top_of_row(s >> 6, cb, vb);
       return t == INVALID ? INVALID : cb + (s & 63u);
     } else {
-      u32 l = lane();
-      for (u32 r = 0; r < ng; r += 64) {
-        u32 i = r + l;
-        u32 b = rblk()[i];  // i < rcap (a multiple of 64): always inside this wave's LDS slice
-        u64 m = ballot(b == blk);  // (groups >= ng hold INVALID: root_clear_from)
-        if (m) return r + (u32)__builtin_ctzll(m);
-      }
-      return INVALID;
+      (void)ng;
+      return uni(gob()[blk]);  // (one LDS read; every block id < ng is a group's)
     }
   }
   // the visible count of block blk's group += delta
@@ -903,6 +900,7 @@ struct WaveGPU {
       rblk()[g] = blk;
       rcnt()[g] = cnt;
       rvis()[g] = vis;
+      gob()[blk] = g;
     }
   }
   // insert a group at index g, shifting [g, ng) up by one: 64-group chunks from the top down, each
@@ -962,7 +960,7 @@ struct WaveGPU {
         u32 jj = i > 0u ? i - 1u : 0u;
         u32 b = rblk()[jj], c = rcnt()[jj], v = rvis()[jj];
         __builtin_amdgcn_wave_barrier();
-        if (i > g && i <= ng) { rblk()[i] = b; rcnt()[i] = c; rvis()[i] = v; }
+        if (i > g && i <= ng) { rblk()[i] = b; rcnt()[i] = c; rvis()[i] = v; gob()[b] = i; }
         __builtin_amdgcn_wave_barrier();
       }
       root_set(g, blk, cnt, vis);
@@ -1065,10 +1063,11 @@ struct WaveGPU {
     leaf = rdlane(lf, k);
     return true;
   }
-  __device__ __forceinline__ void blk_insert(u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+  // a 64-slot directory row, one slot per lane (requested early by split_at: see blk_insert)
+  __device__ __forceinline__ u32 row_ld(const u32* p) const { return *(const u32*)(p + lane()); }
+  // insert (leaf, vis) at slot i of a block whose rows ol / ov (row_ld) hold cnt slots
+  __device__ __forceinline__ void blk_insert(u32 ol, u32 ov, u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
     u32 l = lane();
-    u32 ol = *(u32*)(dl + l);
-    u32 ov = *(u32*)(dv + l);
     u32 sl = shfl(ol, l - 1), sv = shfl(ov, l - 1);
     u32 nlf = l < i ? ol : (l == i ? leaf : sl);
     u32 nvs = l < i ? ov : (l == i ? vis : sv);
