@@ -15,7 +15,7 @@ for L in $OLD $NEW $OLD $NEW; do
   CRDT_GPU_LIB=$L timeout -k 10 120 python scripts/prof_replay.py --docs 8192 --clean | tail -1 || exit 1
 done
 for L in $OLD $NEW; do
-  echo -n "c4-16384 $(basename $L) "
-  CRDT_GPU_LIB=$L timeout -k 10 120 python scripts/prof_replay.py --docs 16384 --random 20000 --clean | tail -1 || exit 1
+  echo -n "c5-1024 $(basename $L) "
+  CRDT_GPU_LIB=$L timeout -k 10 200 python scripts/prof_replay.py --docs 1024 --config5 --clean | tail -1 || exit 1
 done
 [ -z "$MICRO" ] || TAG=_$TAG bash scripts/gpu_micro_paths.sh

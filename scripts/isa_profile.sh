@@ -27,6 +27,21 @@ e = EmuDoc(32)
 if '$TRACE' == 'config4':  # generated ops (bench_config4.py's shape, one document)
     assert e.run_random(e.agent('gen'), 20000, 0xC0FFEE, 64) == 0
     print(20000)
+elif '$TRACE' == 'config5':  # one config-5 history (SURVEY 8(d) shape)
+    sys.path.insert(0, '$ROOT/tests')
+    from fuzz_gen import config5_wire
+    sys.path.insert(0, '$ROOT')
+    from bench import wire_ops
+    w = config5_wire(7, base_len=1 << 20, n_agents=16, rounds=64, ops=64)
+    assert e.run_wire(w, 64) == 0
+    print(wire_ops(w)[0])
+elif '$TRACE'.endswith('.rtx.gz'):  # a wire file (e.g. data/micro/*.rtx.gz): ops = its RemoteOps
+    import gzip, os
+    sys.path.insert(0, '$ROOT')
+    from bench import wire_ops
+    w = gzip.open(os.path.join('$ROOT', '$TRACE'), 'rb').read()
+    assert e.run_wire(w, 64) == 0
+    print(wire_ops(w)[0])
 else:
     assert e.run_wire(load_remote_wire('$TRACE'), 64) == 0
     t = load_trace('$TRACE')

@@ -198,6 +198,26 @@ struct WaveCPU {
   u32 delete_scan(u32 b0, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
     return delete_scan_b(rb, b0, nv, remote, compact, agent, delta);
   }
+  u32 frontier_advance(u32* f, u32 nfr, u32 f0, const u32* pp, u32 np, u32 p0, u32 first, u32 last, u32 cap,
+                       u32& nf0) const {
+    std::vector<u32> h(nfr);
+    for (u32 k = 0; k < nfr; k++) h[k] = k == 0 ? f0 : f[k];
+    for (u32 k = 0; k < nfr; k++) if (h[k] == first) return 0u;
+    auto has = [&](u32 x) {
+      if (np == 0) return false;
+      if (p0 == x) return true;
+      for (u32 j = 1; j < np; j++) if (pp[j] == x) return true;
+      return false;
+    };
+    std::vector<u32> kept;
+    for (u32 k = 0; k < nfr; k++) if (!has(h[k])) kept.push_back(h[k]);
+    u32 m = (u32)kept.size();
+    if (m + 1u > cap) return INVALID;
+    nf0 = m ? kept[0] : last;
+    for (u32 k = 1; k < m; k++) f[k] = kept[k];
+    if (m) f[m] = last;
+    return m + 1u;
+  }
   u32 front_scan(u32 b0, u32 nv, u32 agent, u32 len) const {
     u32 n = 1;
     for (u32 j = b0 + 1; j < nv; j++) {

@@ -548,9 +548,6 @@ struct Replayer {
   // extra_vis: visible items the caller puts into the new leaf's padding slots in HBM itself
   // (counted in its directory slot, its group and the document length here)
   CRDT_HD u32 split_at(u32 idx, u32 padding, u32 extra_vis = 0u) {
-    // the directory block's rows are requested first: their latency overlaps the leaf move
-    u32 blk = g(C_BLK), i = g(C_I);
-    u32 rl = w.row_ld(dleaf(blk)), rv = w.row_ld(dvis(blk));
     u32 nl = g(S_N_LEAVES);
     p(S_N_LEAVES, nl + 1);
     u32 n = g(C_N);
@@ -563,6 +560,7 @@ struct Replayer {
     p(C_N, idx);
     p(C_DIRTY, 1u);
     // link nl right after the cached leaf (directory block insert; the block splits when full)
+    u32 blk = g(C_BLK), i = g(C_I);
     u32 ng = g(S_NG);
     u32 gg = w.root_find_blk(ng, blk);
     u32 cnt = w.root_cnt(gg);
@@ -575,10 +573,8 @@ struct Replayer {
       p(S_NG, ng + 1);
       if (i >= 32) { blk = nb; i -= 32; gg = gg + 1; p(C_BLK, nb); p(C_I, i); }
       cnt = 32;
-      rl = w.row_ld(dleaf(blk));  // (the rows changed: rare)
-      rv = w.row_ld(dvis(blk));
     }
-    w.blk_insert(rl, rv, dleaf(blk), dvis(blk), cnt, i + 1, nl, stolen + extra_vis, sol(), blk);
+    w.blk_insert(w.row_ld(dleaf(blk)), w.row_ld(dvis(blk)), dleaf(blk), dvis(blk), cnt, i + 1, nl, stolen + extra_vis, sol(), blk);
     // the cached leaf's directory count loses `stolen` (moved to nl); group total unchanged
     w.root_set(gg, blk, cnt + 1, w.root_vis(gg) + extra_vis);
     if (extra_vis) inc(S_LEN, extra_vis);
@@ -941,6 +937,15 @@ struct Replayer {
         if (f0 == first) return ST_FRONTIER;
         if (par_contains(pp, np, p0, f0)) p(T_FR0, last);
         else { w.st(f + 1, last); p(S_N_FR, 2); }
+      } else if (nfr <= 64u && np <= 64u) {
+        // lane-parallel (one head / one parent per lane): heads that name `first` make the txn a
+        // duplicate; heads among the parents go, the rest stay in order, `last` joins
+        u32 nf0;
+        u32 r = w.frontier_advance(f, nfr, f0, pp, np, p0, first, last, g(K_FR), nf0);
+        if (r == 0u) return ST_FRONTIER;
+        if (r == INVALID) return ST_CAPACITY;  // (fits() reserved room for nfr + 1 heads)
+        p(S_N_FR, r);
+        p(T_FR0, nf0);
       } else {
         for (u32 k = 0; k < nfr; k++) if ((k == 0 ? f0 : w.ld(f + k)) == first) return ST_FRONTIER;
         u32 m = 0, nf0 = f0;

@@ -652,6 +652,31 @@ struct WaveGPU {
     uint4 v = rec_lane_load(p, nv);
     return delete_scan_r(v.x, v.y, v.z, v.w, 0u, nv, remote, compact, agent, delta);
   }
+  // advance_branch_by for a remote txn (doc.rs:34-48), one frontier head and one parent per lane
+  // (nfr, np <= 64): head 0 is f0 (the write-back tail), heads 1.. live at f[1..].  Returns 0 if a
+  // head is `first` (the txn is known), INVALID if the new frontier would pass cap, else the new
+  // head count: the heads not among the parents (p0, then pp[1..np)) in order, then
+  // `last`; the first of them in nf0, the others at f[1..].
+  __device__ __forceinline__ u32 frontier_advance(u32* f, u32 nfr, u32 f0, const u32* pp, u32 np, u32 p0, u32 first,
+                                                  u32 last, u32 cap, u32& nf0) const {
+    u32 l = lane();
+    bool in = l < nfr;
+    u32 fv = f[in ? l : 0u];
+    fv = l == 0u ? f0 : fv;
+    if (ballot(in && fv == first)) return 0u;
+    u32 pv = pp[l < np ? l : 0u];  // (parent 0 is p0: pp[0] is not written yet)
+    pv = l == 0u ? p0 : pv;
+    bool hit = false;
+    for (u32 j = 0; j < np; j++) hit |= fv == rdlane(pv, j);
+    u64 keep = ballot(in && !hit);
+    u32 m = (u32)__popcll(keep);
+    if (m + 1u > cap) return INVALID;
+    nf0 = m ? rdlane(fv, (u32)__builtin_ctzll(keep)) : last;
+    u32 at = (u32)__popcll(keep & ((1ull << l) - 1ull));  // this head's place in the new frontier
+    if (((keep >> l) & 1ull) && at >= 1u) f[at] = fv;
+    if (m) f[m] = last;  // (every lane stores the same value)
+    return m + 1u;
+  }
   // runs {key0 + j, t0 - j, 1} for j < cnt (backspaced deletes), lane-parallel
   __device__ __forceinline__ void st_del_run(DelRun* p, u32 cnt, u32 key0, u32 t0) const {
     for (u32 j = lane(); j < cnt; j += 64) {
