@@ -44,11 +44,23 @@ st = e.run()
 e.publish_async()
 e.sync()
 e.fit()  # as bench.py: capacities = the stream's use
+replay_ms = e.timings()[0]  # (the growth loop's last launch: without --clean not a full replay)
 if a.clean:
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    ev = [C.c_void_p() for _ in range(2)]
+    for x in ev:
+        hip.hipEventCreate(C.byref(x))
+    s_ = C.c_void_p(e.stream())
     e.reset_async()
+    hip.hipEventRecord(ev[0], s_)
     e.run_async()
+    hip.hipEventRecord(ev[1], s_)
     e.sync()
+    ms = C.c_float()
+    hip.hipEventElapsedTime(C.byref(ms), ev[0], ev[1])
+    replay_ms = ms.value  # the clean launch, HIP events on the engine stream (as bench.py)
     st = e.status()
 e.publish_async()
 e.sync()
-print("status ok:", bool((st == 0).all()), "replay_ms", e.timings()[0], "wall", time.time() - t0)
+print("status ok:", bool((st == 0).all()), "replay_ms", replay_ms, "wall", time.time() - t0)

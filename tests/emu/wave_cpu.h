@@ -76,6 +76,11 @@ struct WaveCPU {
     return -1;
   }
   i32 search_arun(const ARun* b, u32 n, u32 x) const { return search(b, n, x); }
+  template <class T> i32 search_run(const T* b, u32 n, u32 x, T& out) const {
+    i32 k = search(b, n, x);
+    if (k >= 0) out = b[k];
+    return k;
+  }
   i32 search_cwo(const CwoRun* b, u32 n, u32 x) const { return search(b, n, x); }
   DDBlk ld_ddblk(const DDBlk* p) const { return *p; }
   void st_ddblk(DDBlk* p, const DDBlk& v) const { *p = v; }
@@ -110,7 +115,9 @@ struct WaveCPU {
   void cset(u32 i, const Span& s) { c[i & 63] = s; }
   template <class F> void cset_lanes(u32 a, u32 b, F f) { for (u32 l = a; l < b && l < 64; l++) c[l] = f(l); }
   u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
-  u32 scan_batch(u32 a, u32 n, u32 X, u32 orr, u32 my_rank, const u16* oag, const AgentRec* agents, u32 tkey,
+  void rank_load(const AgentRec*, u32) const {}
+  u32 rank_of(const AgentRec* agents, u32, u32 a) const { return agents[a].rank; }
+  u32 scan_batch(u32 a, u32 n, u32 X, u32 orr, u32 my_rank, const u16* oag, const AgentRec* agents, u32 n_agents, u32 tkey,
                  u32 tlen, u32 tagent, u32& last, u32& last_scan) const {
     auto agent_of = [&](u32 o) -> u32 { return o - tkey < tlen ? tagent : oag[o]; };
     u32 f = n;

@@ -37,8 +37,13 @@ constexpr u32 GROUP = 64;                 // directory slots per block (one wave
 constexpr u32 ROOT_CAP_MIN = 256;
 constexpr u32 ROOT_CAP_MAX = 13632;       // floor(163840 / 12 / 64) * 64 (two-level root's top entries)
 // The flat LDS root also keeps a block -> group map (4 B per group: 16 B per group in all), so its
-// largest class is floor(163840 / 16 / 64) * 64 groups; documents past it use the two-level root.
-constexpr u32 ROOT_CAP_LDS = 10240;
+// largest class is floor((163840 - 4 * RANK_LDS) / 16 / 64) * 64 groups; documents past it use
+// the two-level root.
+constexpr u32 ROOT_CAP_LDS = 10176;
+// Agent ranks (the integrate tie-break's name order, doc.rs:207) of documents with at most
+// RANK_LDS agents sit in LDS next to the root while a wave replays (integrate's scan reads one per
+// scanned entry); documents with more read them from HBM.
+constexpr u32 RANK_LDS = 64;
 // Past it the root has two levels (wave_gpu.h HR): LDS top entries of rows that hold 32..64 groups
 // each in HBM, up to ROOT_CAP_MAX - 64 top entries (LDS: 12 B each + two words) -- over 434k
 // groups, 13.9M leaves, 445M entries at the release layout.

@@ -94,10 +94,10 @@ inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
 // Launch shape of a wave-per-document kernel whose waves hold an LDS root of `rcap` groups:
 // up to 4 waves per workgroup within the 160 KiB a workgroup may declare.
 // (flat root: blk / cnt / vis + the block -> group map, 16 B per group; hr: the two-level root:
-// rcap top entries of 12 B + two words per wave)
+// rcap top entries of 12 B + two words per wave; both + RANK_LDS agent ranks)
 struct LaunchShape { u32 wpb, rcap; size_t lds; };
 inline LaunchShape launch_shape(u32 rcap, bool hr = false) {
-  u32 per_wave = hr ? 12u * rcap + 8u : 16u * rcap;
+  u32 per_wave = (hr ? 12u * rcap + 8u : 16u * rcap) + 4u * RANK_LDS;  // (+ the agent ranks)
   u32 wpb = std::max<u32>(1u, std::min<u32>(WAVES_PER_BLOCK, 163840u / per_wave));
   return LaunchShape{wpb, rcap, (size_t)wpb * per_wave};
 }

@@ -49,8 +49,9 @@ __device__ __forceinline__ u32 span_of_order(const PubOut& O, const DocSeg& seg,
 
 #define WAVES_PER_BLOCK 4
 
-// Dynamic LDS of the wave-per-document kernels: each wave's directory root, 3 x rcap u32
-// (launch shape: engine.hip launch_shape).
+// Dynamic LDS of the wave-per-document kernels: each wave's directory root (flat: 4 x rcap u32;
+// two-level: 3 x rcap + 2) and the document's agent ranks (RANK_LDS u32; launch shape:
+// engine.hip launch_shape).
 extern __shared__ u32 s_dyn[];
 template <int L, bool HR = false>
 __device__ __forceinline__ WaveGPU<L, HR> wave_with_root(u32 rcap) {
@@ -58,7 +59,9 @@ __device__ __forceinline__ WaveGPU<L, HR> wave_with_root(u32 rcap) {
   // the LDS address space survives into the member: root accesses are ds_* (lgkmcnt only);
   // a generic pointer would make them flat ops, whose waits also drain every pending store
   w.rcap = rcap;
-  w.rt = (typename WaveGPU<L, HR>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * (HR ? 3u * rcap + 2u : 4u * rcap));
+  u32 root = HR ? 3u * rcap + 2u : 4u * rcap;
+  w.rt = (typename WaveGPU<L, HR>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * (root + RANK_LDS));
+  w.rk = w.rt + root;
   return w;
 }
 // Document of the calling wave: wave k of the launch takes list[k] (or k without a list).

@@ -86,6 +86,9 @@ enum : u32 {
   T_FR0,
   T_AG_ID, T_AG_BASE, T_AG_CNT, T_AG_CAP,
   T_AGL_KEY, T_AGL_ORDER, T_AGL_LEN,
+  // the last non-author agent seq_to_order looked up: its item_orders runs (base, count).  Valid
+  // while that agent authors nothing (use_agent drops it when it becomes the author).
+  T_OA_ID, T_OA_BASE, T_OA_CNT,
   N_SLOTS
 };
 static_assert(K_AGMAP < 64, "read-only slots live in the first context register");
@@ -199,6 +202,7 @@ struct Replayer {
     p(T_FR0, ROOT_ORDER);
     p(T_AG_ID, INVALID); p(T_AG_BASE, 0); p(T_AG_CNT, 0); p(T_AG_CAP, 0);
     p(T_AGL_KEY, 0); p(T_AGL_ORDER, 0); p(T_AGL_LEN, 0);
+    p(T_OA_ID, INVALID); p(T_OA_BASE, 0); p(T_OA_CNT, 0);
     p(T_RB_BASE, 0x80000000u);  // pos - rb_base >= 64 for every valid pos
     p(F_FAST, 0);
     p(F_PRE, 0);
@@ -235,6 +239,7 @@ struct Replayer {
   }
   CRDT_HD void begin() {
     w.root_load(groups(), g(S_NG));
+    w.rank_load(agents(), g(S_N_AGENTS));
     u32 n = g(S_N_CWO);
     if (n) {
       CwoRun r = w.ld_cwo(w.at(cwo(), n - 1));
@@ -687,6 +692,7 @@ struct Replayer {
   // ------------------------------------------------------------------ RLE side tables
   CRDT_HD void use_agent(u32 a) {  // agent cache (author of the current txn)
     if (a == g(T_AG_ID)) return;
+    if (a == g(T_OA_ID)) p(T_OA_ID, INVALID);  // (its run count changes from now on)
     flush_agent();
     p(T_AG_ID, a);
     AgentRec r = w.ld_agent(w.at(agents(), a));
@@ -704,7 +710,7 @@ struct Replayer {
     use_agent(agent);
     return g(T_AG_CNT) ? g(T_AGL_KEY) + g(T_AGL_LEN) : 0u;
   }
-  CRDT_HD bool seq_to_order(u32 agent, u32 seq, u32& order) const {  // doc.rs:26-29
+  CRDT_HD bool seq_to_order(u32 agent, u32 seq, u32& order) {  // doc.rs:26-29
     u32 base, cnt;
     if (agent == g(T_AG_ID)) {
       u32 key = g(T_AGL_KEY);
@@ -714,15 +720,17 @@ struct Replayer {
       }
       base = g(T_AG_BASE);
       cnt = g(T_AG_CNT);
+    } else if (agent == g(T_OA_ID)) {
+      base = g(T_OA_BASE);
+      cnt = g(T_OA_CNT);
     } else {
       AgentRec A = w.ld_agent(w.at(agents(), agent));
       base = A.run_base;
       cnt = A.run_cnt;
+      p(T_OA_ID, agent); p(T_OA_BASE, base); p(T_OA_CNT, cnt);
     }
-    ARun* ar = arun() + base;
-    i32 k = w.search_arun(ar, cnt, seq);
-    if (k < 0) return false;
-    ARun r = w.ld_arun(ar + k);
+    ARun r;
+    if (w.search_run(arun() + base, cnt, seq, r) < 0) return false;
     order = r.order + (seq - r.key);
     return true;
   }
@@ -733,9 +741,8 @@ struct Replayer {
       seq = g(T_CWO_SEQ) + (order - key);
       return true;
     }
-    i32 k = w.search_cwo(cwo(), n, order);
-    if (k < 0) return false;
-    CwoRun r = w.ld_cwo(w.at(cwo(), (u32)k));
+    CwoRun r;
+    if (w.search_run(cwo(), n, order, r) < 0) return false;
     agent = r.agent;
     seq = r.seq + (order - r.key);
     return true;
@@ -748,9 +755,9 @@ struct Replayer {
       agent = w.ld16(w.at(oag(), order));
       return true;
     }
-    i32 k = w.search_cwo(cwo(), n, order);
-    if (k < 0) return false;
-    agent = w.ld_cwo(w.at(cwo(), (u32)k)).agent;
+    CwoRun r;
+    if (w.search_run(cwo(), n, order, r) < 0) return false;
+    agent = r.agent;
     return true;
   }
   // The order -> agent map, if kept, is written when a client_with_order run is retired (a new
@@ -995,7 +1002,7 @@ struct Replayer {
     return ST_OK;
   }
 
-  CRDT_HD i32 id_to_order(u32 agent, u32 seq, u32& order) const {  // doc.rs:236-240
+  CRDT_HD i32 id_to_order(u32 agent, u32 seq, u32& order) {  // doc.rs:236-240
     if (agent == ROOT_AGENT) { order = ROOT_ORDER; return ST_OK; }
     if (agent >= g(S_N_AGENTS)) return ST_UNKNOWN_AGENT;
     if (!seq_to_order(agent, seq, order)) return ST_UNKNOWN_ID;
@@ -1174,7 +1181,8 @@ struct Replayer {
           if (!first_step) {
             if (g(K_AGMAP)) {
               u32 nn = g(C_N), last, last_scan;
-              u32 f = w.scan_batch(c.idx, nn, item.ol, item.orr, w.ld(&w.at(agents(), agent)->rank), oag(), agents(),
+              u32 na = g(S_N_AGENTS);
+              u32 f = w.scan_batch(c.idx, nn, item.ol, item.orr, w.rank_of(agents(), na, agent), oag(), agents(), na,
                                    g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT), last, last_scan);
               if (last != INVALID) {
                 scanning = last_scan != 0u;
@@ -1200,8 +1208,8 @@ struct Replayer {
           if (r == 0) {
             u32 oa;
             if (!order_to_agent(oe.order, oa)) return ST_UNKNOWN_ID;
-            u32 my_rank = w.ld(&w.at(agents(), agent)->rank);
-            u32 other_rank = w.ld(&w.at(agents(), oa)->rank);
+            u32 my_rank = w.rank_of(agents(), g(S_N_AGENTS), agent);
+            u32 other_rank = w.rank_of(agents(), g(S_N_AGENTS), oa);
             if (my_rank > other_rank) scanning = false;
             else if (item.orr == oe.orr) break;
             else { scanning = true; scan_start = c; }

@@ -131,6 +131,7 @@ struct WaveGPU {
   // is ever indexed by a run-time group number.
   typedef __attribute__((address_space(3))) u32 lds_u32;  // ds_read/ds_write, never flat
   lds_u32* rt = nullptr;
+  lds_u32* rk = nullptr;  // agent ranks (documents with <= RANK_LDS agents)
   u32 rcap = 0;
   u32* hrow = nullptr;  // HR: this document's rows (192 u32 each: blk[64], cnt[64], vis[64])
   u32* gsob = nullptr;  // HR: block -> row << 6 | slot
@@ -240,6 +241,34 @@ struct WaveGPU {
     u32 key = ((const u32*)&r)[0];
     u32 len = rlen(r);
     return (needle < key + len) ? (i32)k : -1;
+  }
+  // As search, and the run itself: the last level loads each lane's whole 16 B run, so the caller
+  // needs no second (dependent) load for the run it found.
+  template <class T>
+  __device__ __forceinline__ i32 search_run(const T* base, u32 n, u32 needle, T& out) const {
+    static_assert(sizeof(T) == 16, "16 B runs");
+    if (n == 0) return -1;
+    u32 lo = 0, hi = n;
+    u32 l = lane();
+    while (hi - lo > 64) {
+      u32 step = (hi - lo + 63) / 64;
+      u32 idx = lo + l * step;
+      u32 key = *(const u32*)&base[idx < hi ? idx : hi - 1];
+      u64 m = ballot(idx < hi && key <= needle);
+      if (m == 0) return -1;
+      u32 t = 63 - __builtin_clzll(m);
+      lo = lo + t * step;
+      u32 nh = lo + step;
+      hi = nh < hi ? nh : hi;
+    }
+    u32 idx = lo + l;
+    uint4 v = *(const uint4*)&base[idx < hi ? idx : hi - 1];
+    u64 m = ballot(idx < hi && v.x <= needle);
+    if (m == 0) return -1;
+    u32 t = 63 - __builtin_clzll(m);
+    u32 f[4] = {rdlane(v.x, t), rdlane(v.y, t), rdlane(v.z, t), rdlane(v.w, t)};
+    __builtin_memcpy(&out, f, 16);
+    return needle < f[0] + rlen(out) ? (i32)(lo + t) : -1;
   }
   __device__ __forceinline__ static u32 rlen(const ARun& r) { return r.len; }
   __device__ __forceinline__ static u32 rlen(const CwoRun& r) { return r.len; }
@@ -353,8 +382,18 @@ struct WaveGPU {
   // else scanning from it.  Returns the first lane with an event (a break, or an origin_left
   // other than X: a cursor compare) or n; `last` = the last lane before it (INVALID if none),
   // `last_scan` = whether it left scanning on.
+  // the document's agent ranks into LDS (replay start; n agents, fixed during a launch)
+  __device__ __forceinline__ void rank_load(const AgentRec* agents, u32 n) const {
+    u32 l = lane();
+    if (l < n && l < RANK_LDS) rk[l] = *(const u32*)((const char*)agents + (u64)(l * 16u + 12u));
+    __builtin_amdgcn_wave_barrier();
+  }
+  // agent a's rank (uniform a)
+  __device__ __forceinline__ u32 rank_of(const AgentRec* agents, u32 n, u32 a) const {
+    return n <= RANK_LDS ? uni(rk[a]) : ld(&at(agents, a)->rank);
+  }
   __device__ __forceinline__ u32 scan_batch(u32 a, u32 n, u32 X, u32 orr, u32 my_rank, const u16* oag,
-                                            const AgentRec* agents, u32 tkey, u32 tlen, u32 tagent, u32& last,
+                                            const AgentRec* agents, u32 n_agents, u32 tkey, u32 tlen, u32 tagent, u32& last,
                                             u32& last_scan) const {
     // (the replay's register budget is spent: per-lane values are transient, the per-lane tests
     // become lane masks at once, and the rest is scalar mask arithmetic)
@@ -362,7 +401,8 @@ struct WaveGPU {
     u32 o = (l >= a && l < n) ? (u32)eo : rdlane(eo, a);  // (lanes outside read a valid order's entry)
     u32 ag = *(const u16*)((const char*)oag + (u64)(o * 2u));
     ag = o - tkey < tlen ? tagent : ag;  // the client_with_order tail run is not in the map yet
-    u32 rk = *(const u32*)((const char*)agents + (u64)(ag * 16u + 12u));  // AgentRec::rank
+    u32 rk = n_agents <= RANK_LDS ? (u32)this->rk[ag]  // AgentRec::rank, from LDS when it fits
+                                  : *(const u32*)((const char*)agents + (u64)(ag * 16u + 12u));
     u64 lt = ballot(my_rank > rk);
     u64 ev = ballot(eo == orr) | ballot(el != X) | (~lt & ballot(er == orr));
     u64 in = (n >= 64u ? ~0ull : ((1ull << n) - 1ull)) & (~0ull << a);
