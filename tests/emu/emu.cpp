@@ -63,7 +63,7 @@ struct EmuDoc {
   void prepare(const StreamNeeds& nd, bool track, u32 leaf_div) {
     Caps c = plan_caps(nd, (u32)agents.names.size(), track, leaf_div);
     leaves.assign((size_t)c.leaf * L, Span{0, 0, 0, 0});
-    sol.assign(c.leaf, 0);
+    sol.assign(2 * (size_t)c.leaf, 0);  // {slot, successor} per leaf
     dir_leaf.assign((size_t)c.blk * GROUP, 0);
     dir_vis.assign((size_t)c.blk * GROUP, 0);
     leaf_of.assign(std::max<u32>(c.map, 1), 0xDEADBEEFu);
@@ -105,7 +105,7 @@ struct EmuDoc {
     if (need & 1u) {
       u32 nl = seg.leaf_cap * 2 > MAX_LEAVES ? MAX_LEAVES : seg.leaf_cap * 2;
       leaves.resize((size_t)nl * L, Span{0, 0, 0, 0});
-      sol.resize(nl, 0);
+      sol.resize(2 * (size_t)nl, 0);
       seg.leaf_cap = nl;
       seg.blk_cap = blk_cap_for(nl);
       seg.grp_cap = seg.blk_cap;
@@ -283,13 +283,27 @@ int emu_check(void* h, char* msg, int cap) {
       u32 v = 0;
       for (u32 k = 0; k < d->L; k++) v += clen(d->leaves[(size_t)lf * d->L + k]);
       if (v != dv) { snprintf(msg, cap, "group %u slot %u leaf %u: dir_vis %u content %u", g, i, lf, dv, v); return 1; }
-      if (d->sol[lf] != ((G.blk << 6) | i)) { snprintf(msg, cap, "slot_of_leaf[%u]=%x expected blk %u i %u", lf, d->sol[lf], G.blk, i); return 2; }
+      if (d->sol[2 * lf] != ((G.blk << 6) | i)) { snprintf(msg, cap, "slot_of_leaf[%u]=%x expected blk %u i %u", lf, d->sol[2 * lf], G.blk, i); return 2; }
       gsum += dv;
     }
     if (gsum != G.vis) { snprintf(msg, cap, "group %u vis %u sum %llu", g, G.vis, (unsigned long long)gsum); return 3; }
     total += gsum;
   }
   if (total != d->st.len) { snprintf(msg, cap, "len %u total %llu", d->st.len, (unsigned long long)total); return 4; }
+  // the leaf list (slot entries' successor links) follows the directory order
+  u32 prev = INVALID;
+  for (u32 g = 0; g < d->st.ng; g++) {
+    const GroupRec& G = d->groups[g];
+    for (u32 i = 0; i < G.cnt; i++) {
+      u32 lf = d->dir_leaf[(size_t)G.blk * GROUP + i];
+      if (prev != INVALID && d->sol[2 * prev + 1] != lf) {
+        snprintf(msg, cap, "leaf %u: successor link %u, directory successor %u", prev, d->sol[2 * prev + 1], lf);
+        return 5;
+      }
+      prev = lf;
+    }
+  }
+  if (prev != INVALID && d->sol[2 * prev + 1] != END_LEAF) { snprintf(msg, cap, "last leaf %u links %u", prev, d->sol[2 * prev + 1]); return 6; }
   return 0;
 }
 

@@ -33,6 +33,7 @@ struct WaveCPU {
   static u64 clock() { return 0; }
   u32 ld(const u32* p) const { return *p; }
   u32 ld_raw(const u32* p) const { return *p; }
+  void ld_raw2(const u32* p, u32& a, u32& b) const { a = p[0]; b = p[1]; }
   static u32 uni_(u32 x) { return x; }
   void st(u32* p, u32 v) const { *p = v; }
   void st(i32* p, i32 v) const { *p = v; }
@@ -376,14 +377,14 @@ struct WaveCPU {
     for (u32 k = cnt; k > i; k--) { dl[k] = dl[k - 1]; dv[k] = dv[k - 1]; }
     dl[i] = leaf;
     dv[i] = vis;
-    for (u32 k = i; k <= cnt; k++) sol[dl[k]] = (blk << 6) | k;
+    for (u32 k = i; k <= cnt; k++) sol[2 * dl[k]] = (blk << 6) | k;  // ({slot, successor} entries)
   }
   u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
     u32 t = 0;
     for (u32 k = 32; k < 64; k++) {
       ndl[k - 32] = dl[k];
       ndv[k - 32] = dv[k];
-      sol[dl[k]] = (nb << 6) | (k - 32);
+      sol[2 * dl[k]] = (nb << 6) | (k - 32);
       t += dv[k];
     }
     return t;

@@ -253,7 +253,7 @@ struct Pools {
   Span* leaves;        // [leaf][L]
   u32* dir_leaf;       // [blk*64 + i]
   u32* dir_vis;
-  u32* slot_of_leaf;   // [leaf_base + leaf] = blk<<6 | i
+  u32* slot_of_leaf;   // [2 * (leaf_base + leaf)] = blk<<6 | i, [+1] = successor leaf (END_LEAF: last)
   u32* leaf_of;        // [map_base + order]
   u16* agent_of;       // [map_base + order] (DOC_TRACK_AGENT documents)
   CwoRun* cwo;

@@ -342,7 +342,7 @@ struct crdt_engine {
       nseg[d] = s;
     }
     HIPCHK(dalloc(np.leaves, nl * L));
-    HIPCHK(dalloc(np.sol, nl));
+    HIPCHK(dalloc(np.sol, 2 * nl));  // {directory slot, successor leaf} per leaf
     HIPCHK(dalloc(np.dir_leaf, nb * GROUP));
     HIPCHK(dalloc(np.dir_vis, nb * GROUP));
     HIPCHK(dalloc(np.leaf_of, nm));
@@ -359,7 +359,7 @@ struct crdt_engine {
     HIPCHK(dalloc(np.frontier, nfr));
     HIPCHK(dalloc(np.groups, nb));
     HIPCHK(dalloc(np.agents, nag));
-    np.bytes = nl * L * 16 + nl * 4 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) +
+    np.bytes = nl * L * 16 + nl * 8 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) +
                (any_hroot ? nhr * HROOT_ROW * 4 + nb * 4 : 0) + nc * 16 + na * 16 + ndl * 12 +
                ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * 16 + nfr * 4 + nb * 16;
     if (getenv("CRDT_DEBUG_MEM"))

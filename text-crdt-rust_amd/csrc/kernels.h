@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const Do
   DocSeg o = old_seg[d];
   DocSeg w = dst.seg[d];
   bcopy(dst.leaves + w.leaf_base * L, src.leaves + o.leaf_base * L, (u64)s.n_leaves * L);
-  bcopy(dst.slot_of_leaf + w.leaf_base, src.slot_of_leaf + o.leaf_base, s.n_leaves);
+  bcopy(dst.slot_of_leaf + 2 * w.leaf_base, src.slot_of_leaf + 2 * o.leaf_base, 2ull * s.n_leaves);
   bcopy(dst.dir_leaf + w.blk_base * GROUP, src.dir_leaf + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
   bcopy(dst.dir_vis + w.blk_base * GROUP, src.dir_vis + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
   if (w.flags & o.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);

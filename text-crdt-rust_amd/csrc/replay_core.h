@@ -78,7 +78,7 @@ enum : u32 {
   F_BASE,
   // x2: leaf cache bookkeeping
   C_LEAF = 128, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
-  C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order
+  C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order (INVALID: not known)
   // RLE tails
   T_CWO_KEY, T_CWO_AGENT, T_CWO_SEQ, T_CWO_LEN,
   T_DEL_KEY, T_DEL_ORDER, T_DEL_LEN,
@@ -158,7 +158,7 @@ struct Replayer {
     pset(P_LV, P.leaves + sg.leaf_base * (u64)L);
     pset(P_DL, P.dir_leaf + sg.blk_base * (u64)GROUP);
     pset(P_DV, P.dir_vis + sg.blk_base * (u64)GROUP);
-    pset(P_SOL, P.slot_of_leaf + sg.leaf_base);
+    pset(P_SOL, P.slot_of_leaf + 2u * sg.leaf_base);  // {slot, successor} per leaf
     pset(P_LOF, P.leaf_of + sg.map_base);
     pset(P_OAG, P.agent_of + sg.map_base);
     pset(P_CWO, P.cwo + sg.cwo_base);
@@ -234,6 +234,7 @@ struct Replayer {
     w.st(dl(), 0u);
     w.st(dv(), 0u);
     w.st(sol(), 0u);
+    w.st(sol() + 1, END_LEAF);
     w.st(fr(), ROOT_ORDER);
     w.root_init(0u, 1u, 0u);
   }
@@ -322,7 +323,7 @@ struct Replayer {
   // ------------------------------------------------------------------ directory
   CRDT_HD void slot_of(u32 leaf, u32& blk, u32& i) const {
     if (leaf == g(C_LEAF)) { blk = g(C_BLK); i = g(C_I); return; }
-    u32 v = w.ld(w.at(sol(), leaf));
+    u32 v = w.ld(w.template at<2>(sol(), leaf));
     blk = v >> 6;
     i = v & 63u;
   }
@@ -335,14 +336,6 @@ struct Replayer {
   CRDT_HD u32 leaf_at_end() const {
     u32 gg = g(S_NG) - 1;
     return w.ld(dleaf(w.root_blk(gg)) + w.root_cnt(gg) - 1);
-  }
-  CRDT_HD u32 next_leaf(u32 leaf) const {
-    u32 blk, i;
-    slot_of(leaf, blk, i);
-    u32 gg = w.root_find_blk(g(S_NG), blk);
-    if (i + 1 < w.root_cnt(gg)) return w.ld(dleaf(blk) + i + 1);
-    if (gg + 1 < g(S_NG)) return w.ld(dleaf(w.root_blk(gg + 1)));
-    return INVALID;
   }
   // Record the cached leaf's new visible count in the directory.
   CRDT_HD void dir_set_cached_vis(u32 v) {
@@ -376,7 +369,8 @@ struct Replayer {
   }
   // Cache `leaf`; `slot` = its directory slot (blk << 6 | i), possibly a load still in flight:
   // the leaf's entries are requested before the slot is first used, so both arrive together.
-  CRDT_HD void load_cache(u32 leaf, u32 slot) {
+  // `succ`: its successor leaf if the caller has it (INVALID: not known yet).
+  CRDT_HD void load_cache(u32 leaf, u32 slot, u32 succ = INVALID) {
     commit();
     p(C_N, w.cache_load(leafp(leaf)));
     u32 sl = w.uni_(slot);
@@ -388,23 +382,38 @@ struct Replayer {
     p(C_NOW, v);
     p(C_VIS, v);
     p(C_VS_OK, 0);
-    p(C_SUCC, INVALID);
+    p(C_SUCC, w.uni_(succ));
+    p(C_SUCC_ORD, INVALID);
   }
-  // Successor of the cached leaf (INVALID at the end of the document) and its first order,
-  // memoised: only split_at changes it while the cache stays on one leaf.
-  CRDT_HD u32 cached_succ(u32& first_order) {
+  // Successor of the cached leaf (INVALID at the end of the document): each leaf's slot entry
+  // links its successor (the leaf list split_at maintains, as the reference's leaves are linked
+  // in document order), so a leaf walk needs no directory lookup.
+  CRDT_HD u32 cached_succ_leaf() {
     u32 sc = g(C_SUCC);
-    if (sc != INVALID) { first_order = g(C_SUCC_ORD); return sc == END_LEAF ? INVALID : sc; }
-    u32 nl = next_leaf(g(C_LEAF));
-    u32 fo = nl == INVALID ? 0u : w.ld(&leafp(nl)->order);
-    p(C_SUCC, nl == INVALID ? END_LEAF : nl);
-    p(C_SUCC_ORD, fo);
+    if (sc == INVALID) {
+      sc = w.ld(w.template at<2>(sol(), g(C_LEAF)) + 1);
+      p(C_SUCC, sc);
+    }
+    return sc == END_LEAF ? INVALID : sc;
+  }
+  // ... and its first order (loaded once per cached leaf)
+  CRDT_HD u32 cached_succ(u32& first_order) {
+    u32 nl = cached_succ_leaf();
+    if (nl == INVALID) { first_order = 0u; return INVALID; }
+    u32 fo = g(C_SUCC_ORD);
+    if (fo == INVALID) {
+      fo = w.ld(&leafp(nl)->order);
+      p(C_SUCC_ORD, fo);
+    }
     first_order = fo;
     return nl;
   }
   CRDT_HD void ensure(u32 leaf) {
     if (leaf == g(C_LEAF)) return;
-    load_cache(leaf, w.ld_raw(w.at(sol(), leaf)));  // (commits the cached leaf first) slot and entries: one round trip
+    // slot, successor and entries: one round trip (commits the cached leaf first)
+    u32 slot, succ;
+    w.ld_raw2(w.template at<2>(sol(), leaf), slot, succ);  // (one 8-byte load)
+    load_cache(leaf, slot, succ);
   }
   // set entry idx of the cached leaf (tracks the cached visible count exactly)
   CRDT_HD void set(u32 idx, const Span& e) {
@@ -435,8 +444,7 @@ struct Replayer {
   CRDT_HD bool next_entry(Cursor& c) {
     ensure(c.leaf);
     if (c.idx + 1 < g(C_N)) { c.idx++; c.off = 0; return true; }
-    u32 fo;
-    u32 nl = cached_succ(fo);
+    u32 nl = cached_succ_leaf();
     if (nl == INVALID) return false;
     c.leaf = nl;
     c.idx = 0;
@@ -489,7 +497,7 @@ struct Replayer {
       commit();
       u32 lf, blk, i;
       if (!find_by_pos(pos, lf, vs, blk, i)) return false;
-      if (lf != g(C_LEAF)) load_cache(lf, (blk << 6) | i);
+      if (lf != g(C_LEAF)) load_cache(lf, (blk << 6) | i, w.ld_raw(w.template at<2>(sol(), lf) + 1));  // (successor: in flight with the entries)
       p(C_VSTART, vs);
       p(C_VS_OK, 1);
     }
@@ -555,6 +563,10 @@ struct Replayer {
   CRDT_HD u32 split_at(u32 idx, u32 padding, u32 extra_vis = 0u) {
     u32 nl = g(S_N_LEAVES);
     p(S_N_LEAVES, nl + 1);
+    // the leaf list: nl goes right after the cached leaf
+    u32 osucc = cached_succ_leaf();
+    w.st(w.template at<2>(sol(), nl) + 1, osucc == INVALID ? END_LEAF : osucc);
+    w.st(w.template at<2>(sol(), g(C_LEAF)) + 1, nl);
     u32 n = g(C_N);
     u32 stolen = w.cache_vis_from(idx);
     u32 first_moved = w.cget_order(idx);
@@ -586,8 +598,8 @@ struct Replayer {
     u32 cv = g(C_VIS) - stolen;
     w.st(dvis(blk) + i, cv);
     p(C_VIS, cv);
-    p(C_SUCC, padding ? INVALID : nl);  // (with padding the cursor moves to nl next)
-    p(C_SUCC_ORD, first_moved);
+    p(C_SUCC, nl);
+    p(C_SUCC_ORD, padding ? INVALID : first_moved);  // (padding: the caller writes nl's first entries)
     return nl;
   }
   // mutations.rs:17-179 insert_internal.  Items a0..a(n-1) (n <= 3) stay in named registers;

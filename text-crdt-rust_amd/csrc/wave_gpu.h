@@ -149,6 +149,11 @@ struct WaveGPU {
   __device__ __forceinline__ u32 ld(const u32* p) const { return uni(*(const u32*)p); }
   // a load whose wait is deferred to the first uni_() of its value (overlaps later loads)
   __device__ __forceinline__ u32 ld_raw(const u32* p) const { return *(const u32*)p; }
+  __device__ __forceinline__ void ld_raw2(const u32* p, u32& a, u32& b) const {  // p 8-byte aligned
+    uint2 v = *(const uint2*)p;
+    a = v.x;
+    b = v.y;
+  }
   __device__ __forceinline__ static u32 uni_(u32 x) { return uni(x); }
   __device__ __forceinline__ void st(u32* p, u32 v) const { *(u32*)p = v; }
   __device__ __forceinline__ void st(i32* p, i32 v) const { *(i32*)p = v; }
@@ -1139,7 +1144,7 @@ struct WaveGPU {
     if (l >= i && l <= cnt) {
       *(u32*)(dl + l) = nlf;
       *(u32*)(dv + l) = nvs;
-      *(u32*)(sol + nlf) = (blk << 6) | l;
+      *(u32*)(sol + 2u * nlf) = (blk << 6) | l;  // (slot entries are {slot, successor})
     }
   }
   __device__ __forceinline__ u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
@@ -1150,7 +1155,7 @@ struct WaveGPU {
       v = *(const u32*)(dv + l);
       *(u32*)(ndl + l - 32) = lf;
       *(u32*)(ndv + l - 32) = v;
-      *(u32*)(sol + lf) = (nb << 6) | (l - 32);
+      *(u32*)(sol + 2u * lf) = (nb << 6) | (l - 32);
     }
     return wave_sum(v);
   }
