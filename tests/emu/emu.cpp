@@ -82,7 +82,7 @@ struct EmuDoc {
     u32 base = 0;
     for (u32 a = 0; a < agents.names.size(); a++) {
       u32 cap = (a < nd.txns_per_agent.size() ? nd.txns_per_agent[a] : 0) + 1;
-      agent_tab[a] = AgentRec{base, 0, cap, rk[a]};
+      agent_tab[a] = AgentRec{base, 0, cap, rk[a], 0, 0, 0, 0};
       base += cap;
     }
     seg = DocSeg{};

@@ -40,6 +40,7 @@ struct WaveCPU {
   template <class T> T ldT(const T* p) const { return *p; }
   template <class T> void stT(T* p, const T& v) const { *p = v; }
   AgentRec ld_agent(const AgentRec* p) const { return *p; }
+  void st_agent_tail(AgentRec* p, u32 key, u32 order, u32 len) const { p->tkey = key; p->torder = order; p->tlen = len; }
   ARun ld_arun(const ARun* p) const { return *p; }
   void st_arun(ARun* p, const ARun& v) const { *p = v; }
   CwoRun ld_cwo(const CwoRun* p) const { return *p; }

@@ -124,7 +124,10 @@ struct DDRun { u32 key, len, excess; };        // double_deletes
 constexpr u32 DD_BLK = 64;
 struct DDBlk { u32 phys, first, cnt, pad; };   // physical block, first key, entries
 struct TxnRec { u32 order, len, shadow, poff, pn, pad[3]; };  // txns (32 B)
-struct AgentRec { u32 run_base, run_cnt, run_cap, rank; };   // per-document agent table
+// Per-document agent table.  tkey / torder / tlen: a copy of the agent's last item_orders run
+// (valid when run_cnt > 0), written whenever it stops being the replay's current author, so
+// switching authors is one 32 B load instead of the record and then its last run.
+struct AgentRec { u32 run_base, run_cnt, run_cap, rank, tkey, torder, tlen, pad; };
 struct GroupRec { u32 blk, cnt, vis, pad; };   // persisted root level of the directory
 
 // ---------------------------------------------------------------------------------------------

@@ -329,7 +329,7 @@ struct crdt_engine {
         u32 t = a < h.cum.txns_per_agent.size() ? h.cum.txns_per_agent[a] : 0;
         u32 need = std::min<u32>(t + 1, 64 + t / 64);
         if (h.agent_cap[a] < need) h.agent_cap[a] = need;
-        agent_tab.push_back(AgentRec{rb, 0, h.agent_cap[a], rk[a]});
+        agent_tab.push_back(AgentRec{rb, 0, h.agent_cap[a], rk[a], 0, 0, 0, 0});
         rb += h.agent_cap[a];
       }
       s.arun_cap = rb;
@@ -361,7 +361,7 @@ struct crdt_engine {
     HIPCHK(dalloc(np.agents, nag));
     np.bytes = nl * L * 16 + nl * 8 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) +
                (any_hroot ? nhr * HROOT_ROW * 4 + nb * 4 : 0) + nc * 16 + na * 16 + ndl * 12 +
-               ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * 16 + nfr * 4 + nb * 16;
+               ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * (u64)sizeof(AgentRec) + nfr * 4 + nb * 16;
     if (getenv("CRDT_DEBUG_MEM"))
       fprintf(stderr, "layout: leaves %llu blocks %llu map %llu cwo %llu arun %llu del %llu ddblk %llu txn %llu par %llu agents %llu fr %llu -> %.1f MB\n",
               (unsigned long long)nl, (unsigned long long)nb, (unsigned long long)nm, (unsigned long long)nc,

@@ -160,7 +160,13 @@ __global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const Do
     AgentRec an = dst.agents[w.agent_base + a];
     bcopy(dst.arun + w.arun_base + an.run_base, src.arun + o.arun_base + ao.run_base, ao.run_cnt);
     __syncthreads();
-    if (threadIdx.x == 0) dst.agents[w.agent_base + a].run_cnt = ao.run_cnt;
+    if (threadIdx.x == 0) {  // (the run count and the copy of the last run move; base / cap are the new layout's)
+      AgentRec* q = dst.agents + w.agent_base + a;
+      q->run_cnt = ao.run_cnt;
+      q->tkey = ao.tkey;
+      q->torder = ao.torder;
+      q->tlen = ao.tlen;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) dst.st[d].n_agents = new_n_agents[d];

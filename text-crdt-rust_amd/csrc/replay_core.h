@@ -283,7 +283,11 @@ struct Replayer {
   }
   CRDT_HD void flush_agent() {
     u32 a = g(T_AG_ID), cnt = g(T_AG_CNT);
-    if (a != INVALID && cnt) w.st(&w.at(arun(), g(T_AG_BASE) + cnt - 1)->len, g(T_AGL_LEN));
+    if (a != INVALID && cnt) {
+      u32 ln = g(T_AGL_LEN);
+      w.st(&w.at(arun(), g(T_AG_BASE) + cnt - 1)->len, ln);
+      w.st_agent_tail(w.at(agents(), a), g(T_AGL_KEY), g(T_AGL_ORDER), ln);  // (AgentRec tail copy)
+    }
   }
   CRDT_HD void finish() {
     commit();
@@ -707,13 +711,12 @@ struct Replayer {
     if (a == g(T_OA_ID)) p(T_OA_ID, INVALID);  // (its run count changes from now on)
     flush_agent();
     p(T_AG_ID, a);
-    AgentRec r = w.ld_agent(w.at(agents(), a));
+    AgentRec r = w.ld_agent(w.at(agents(), a));  // (with the copy of its last run: no second load)
     p(T_AG_BASE, r.run_base);
     p(T_AG_CNT, r.run_cnt);
     p(T_AG_CAP, r.run_cap);
     if (r.run_cnt) {
-      ARun x = w.ld_arun(w.at(arun(), r.run_base + r.run_cnt - 1));
-      p(T_AGL_KEY, x.key); p(T_AGL_ORDER, x.order); p(T_AGL_LEN, x.len);
+      p(T_AGL_KEY, r.tkey); p(T_AGL_ORDER, r.torder); p(T_AGL_LEN, r.tlen);
     } else {
       p(T_AGL_LEN, 0);  // no runs: the tail test in seq_to_order fails on its own
     }

@@ -172,6 +172,9 @@ struct WaveGPU {
     for (u32 k = 0; k < sizeof(T) / 4; k++) s[k] = o[k];
   }
   __device__ __forceinline__ AgentRec ld_agent(const AgentRec* p) const { return ldT(p); }
+  __device__ __forceinline__ void st_agent_tail(AgentRec* p, u32 key, u32 order, u32 len) const {
+    *(uint4*)&p->tkey = make_uint4(key, order, len, 0u);  // (every lane stores the same values)
+  }
   __device__ __forceinline__ ARun ld_arun(const ARun* p) const { return ldT(p); }
   __device__ __forceinline__ void st_arun(ARun* p, const ARun& v) const { stT(p, v); }
   __device__ __forceinline__ CwoRun ld_cwo(const CwoRun* p) const { return ldT(p); }
@@ -390,7 +393,7 @@ struct WaveGPU {
   // the document's agent ranks into LDS (replay start; n agents, fixed during a launch)
   __device__ __forceinline__ void rank_load(const AgentRec* agents, u32 n) const {
     u32 l = lane();
-    if (l < n && l < RANK_LDS) rk[l] = *(const u32*)((const char*)agents + (u64)(l * 16u + 12u));
+    if (l < n && l < RANK_LDS) rk[l] = agents[l].rank;
     __builtin_amdgcn_wave_barrier();
   }
   // agent a's rank (uniform a)
@@ -407,7 +410,7 @@ struct WaveGPU {
     u32 ag = *(const u16*)((const char*)oag + (u64)(o * 2u));
     ag = o - tkey < tlen ? tagent : ag;  // the client_with_order tail run is not in the map yet
     u32 rk = n_agents <= RANK_LDS ? (u32)this->rk[ag]  // AgentRec::rank, from LDS when it fits
-                                  : *(const u32*)((const char*)agents + (u64)(ag * 16u + 12u));
+                                  : *(const u32*)((const char*)agents + (u64)(ag * (u32)sizeof(AgentRec) + 12u));
     u64 lt = ballot(my_rank > rk);
     u64 ev = ballot(eo == orr) | ballot(el != X) | (~lt & ballot(er == orr));
     u64 in = (n >= 64u ? ~0ull : ((1ull << n) - 1ull)) & (~0ull << a);
