@@ -19,7 +19,8 @@ import sys
 
 SYM = "_ZN4crdt8k_replayILi32EEEvNS_5PoolsEjjjPKj"
 FILTER = int(os.environ.get("FILTER_CALL_LINE", "0"))
-FN = os.environ.get("FILTER_FN", "")  # print this function's instructions (address, count/op)
+FN = os.environ.get("FILTER_FN", "")
+DUMP = open(os.environ["DUMP_ADDR"], "w") if os.environ.get("DUMP_ADDR") else None  # per-instruction counts  # print this function's instructions (address, count/op)
 MNS = tuple(x for x in os.environ.get("FILTER_MN", "").split(",") if x)  # only these mnemonic prefixes  # only code inlined from a call at this line
 
 
@@ -268,6 +269,8 @@ def main():
                     else "lane" if mn.startswith(("v_readlane", "v_writelane", "v_readfirstlane"))
                     else "valu" if mn.startswith("v_") else "mem")
             fn = ch[-1].name if ch else SYM
+            if DUMP is not None:
+                DUMP.write(f"{a:#x} {cnt / float(sys.argv[6]):.6f} {mn} {fl}:{ln}\n")
             if FN and FN in fn:
                 print(f"  {a:#x} {cnt / float(sys.argv[6]):6.3f} {mn:24s} {fl}:{ln}")
             kinds[kind] += cnt
