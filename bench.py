@@ -215,6 +215,20 @@ def golden(trace: str, key: str):
         return None
 
 
+def golden_pos_seq(trace: str):
+    """Committed fixture (tests/golden/ap_remote_pos_seq.delta.gz, made by make_queries.py from the
+    oracle): seq of the item at every visible position of the trace's remote replay (one author,
+    agent 0), or None."""
+    import gzip
+    if trace != "automerge-paper":
+        return None
+    try:
+        d = np.frombuffer(gzip.open(os.path.join(ROOT, "tests", "golden", "ap_remote_pos_seq.delta.gz")).read(), np.int32)
+    except OSError:
+        return None
+    return np.cumsum(d.astype(np.int64)).astype(np.uint32)
+
+
 TRAFFIC_WORKLOAD = {"k_replay": "automerge-paper remote, one clean launch",
                     "k_materialize": "automerge-paper remote, per-document content copies, one launch"}
 
@@ -332,6 +346,9 @@ def stated_size_leg(args, wire, n_ops_doc, hip, docs=4096, steps=3):
     gold = golden(args.trace, "remote_digest")
     ok = bool((e.status() == 0).all()) and (gold is None or bool((e.digests() == np.uint64(int(gold, 16))).all()))
     ok = ok and (not q or bool(((d_p2 == d_pos) & (d_del == 0)).all().item()))
+    gseq = golden_pos_seq(args.trace)
+    if q and gseq is not None and int(lens.min()) == gseq.shape[0] == int(lens.max()):
+        ok = ok and bool((d_seq == torch.from_numpy(gseq.view(np.int32)).to(dev)[d_pos.long()]).all().item())
     e.close()
     return {"docs_per_gpu": docs, "waves_per_simd": docs / SIMDS, "steps": steps, "ms_per_step": el / steps * 1e3,
             "value": docs * n_ops_doc * steps / el, "k_replay_ms": float(np.mean(ms)), "parity_ok": ok,
@@ -484,6 +501,12 @@ def main():
     st = eng.status()
     ok = bool((st == 0).all())
     q_ok = bool(((d_p2 == d_pos) & (d_del == 0) & (d_ag == 0)).all().item()) if q else True
+    gseq = golden_pos_seq(args.trace)  # every timed pos -> loc answer against the oracle's (fixture)
+    q_gold = None
+    if q and gseq is not None and int(lens.min()) == gseq.shape[0] == int(lens.max()):
+        g = torch.from_numpy(gseq.view(np.int32)).to(dev)
+        q_gold = bool((d_seq == g[d_pos.long()]).all().item())
+        q_ok = q_ok and q_gold
     dg = eng.digests()
     t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, torch.device("cpu") if args.share_gpu else dev)
     gold = golden(args.trace, "remote_digest")
@@ -536,7 +559,9 @@ def main():
             "cpu_baseline": cpu,
             "parity_ok": ok,
             "parity": "every document's digest == committed oracle golden digest (tests/golden); every timed "
-                      "pos->loc answer round-trips through loc->pos",
+                      "pos->loc answer == the oracle's (tests/golden/ap_remote_pos_seq.delta.gz) and round-trips "
+                      "through loc->pos",
+            "queries_vs_oracle_fixture": q_gold,
             "queries_ok": q_ok,
             "world_size": dist.get_world_size() if dist is not None else 1,
             "per_rank_ops_s": [n_ops_doc * n * args.steps / t for t in per_rank],

@@ -294,3 +294,19 @@ def test_splitlist_index_concurrent(seed):
         assert sa == sb
         if sa == 0:
             assert a.digest() == b.digest()
+
+
+def test_query_fixture_matches_oracle():
+    # tests/golden/ap_remote_pos_seq.delta.gz (bench.py checks every timed pos -> loc answer against
+    # it) is the oracle's pos -> (agent 0, seq) for every position of automerge-paper's remote replay
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import golden_pos_seq
+    from crdt_amd.traces import load_remote_wire
+    o = OracleDoc(32, 16)
+    assert o.apply_remote_wire(load_remote_wire("automerge-paper")) == 0
+    gseq = golden_pos_seq("automerge-paper")
+    assert gseq is not None and gseq.shape[0] == len(o)
+    a, s = o.pos_to_loc(np.arange(len(o), dtype=np.uint32))
+    assert (a == 0).all() and np.array_equal(s, gseq)
