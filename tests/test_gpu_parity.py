@@ -450,3 +450,37 @@ def test_kevin_debug_layout_two_level_root():
     assert_same(g, o.export())
     assert int(e.digests()[0]) == o.digest()
     check_queries_sampled(e, 0, o)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_front_runs_mixed(seed):
+    # runs of local inserts at position 0 (leaf_insert_front's closed form: the prepends that fit
+    # the first leaf in one lane-parallel write; the one that finds it full splits at index 0) of
+    # 1-3 chars, broken by deletes at the front (the next run's origin_right is then a deleted item),
+    # typing elsewhere, and runs longer than the record window -- bit-exact vs the oracle at both
+    # layouts, with queries (tests/test_emu_parity.py runs the same shapes on the CPU emulation)
+    rng = np.random.default_rng(100 + seed)
+    counts, patches, ln = [], [], 0
+    while len(counts) < 20000:
+        k, w = int(rng.integers(1, 150)), int(rng.integers(1, 4))
+        for _ in range(k):
+            counts.append(1); patches.append((0, 0, w)); ln += w
+        r = rng.random()
+        if r < 0.4 and ln > 3:
+            d = int(rng.integers(1, 4))
+            counts.append(1); patches.append((0, d, 0)); ln -= d
+        elif r < 0.7:
+            pos = int(rng.integers(0, ln + 1))
+            for j in range(int(rng.integers(1, 6))):
+                counts.append(1); patches.append((pos + j, 0, 1)); ln += 1
+    c = np.array(counts, np.uint32)
+    p = np.array(patches, np.uint32).reshape(-1, 3)
+    for L in (32, 4):
+        e = crdt_amd.Engine(1, L)
+        a = e.agent_intern([0], ["seph"])
+        assert e.apply_trace([0], int(a[0]), c, p)[0] == 0
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        assert o.apply_trace(o.agent("seph"), c, p) == 0
+        assert_same(e.export(0), o.export())
+        assert int(e.digests()[0]) == o.digest()
+        check_queries_sampled(e, 0, o, n=1 << 14)
