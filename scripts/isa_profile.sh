@@ -27,6 +27,12 @@ e = EmuDoc(32)
 if '$TRACE' == 'config4':  # generated ops (bench_config4.py's shape, one document)
     assert e.run_random(e.agent('gen'), 20000, 0xC0FFEE, 64) == 0
     print(20000)
+elif '$TRACE' == 'kevin':  # 200k single-char prepends (benches/yjs.rs:51-62 shape)
+    import numpy as np
+    n = 200000
+    c = np.ones(n, np.uint32); pt = np.zeros((n, 3), np.uint32); pt[:, 2] = 1
+    assert e.run_local(e.agent('seph'), c, pt, 64) == 0
+    print(n)
 elif '$TRACE' == 'config5':  # one config-5 history (SURVEY 8(d) shape)
     sys.path.insert(0, '$ROOT/tests')
     from fuzz_gen import config5_wire

@@ -712,7 +712,7 @@ struct WaveGPU {
     u32 fv = f[in ? l : 0u];
     fv = l == 0u ? f0 : fv;
     if (ballot(in && fv == first)) return 0u;
-    u32 pv = pp[l < np ? l : 0u];  // (parent 0 is p0: pp[0] is not written yet)
+    u32 pv = np > 1u ? pp[l < np ? l : 0u] : 0u;  // (parent 0 is p0: pp[0] is not written yet)
     pv = l == 0u ? p0 : pv;
     bool hit = false;
     for (u32 j = 0; j < np; j++) hit |= fv == rdlane(pv, j);
