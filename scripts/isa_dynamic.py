@@ -21,6 +21,8 @@ SYM = "_ZN4crdt8k_replayILi32EEEvNS_5PoolsEjjjPKj"
 FILTER = int(os.environ.get("FILTER_CALL_LINE", "0"))
 FN = os.environ.get("FILTER_FN", "")
 DUMP = open(os.environ["DUMP_ADDR"], "w") if os.environ.get("DUMP_ADDR") else None  # per-instruction counts  # print this function's instructions (address, count/op)
+LANE_CALLERS = os.environ.get("LANE_CALLERS")  # also rank context lane reads/writes by the line that asked for them
+HELPER = re.compile(r"(E1gEj$|E1pEjj$|E3incEjj$|2xgEj$|2xsEjj$|6rdlaneE|6wrlaneE)")
 MNS = tuple(x for x in os.environ.get("FILTER_MN", "").split(",") if x)  # only these mnemonic prefixes  # only code inlined from a call at this line
 
 
@@ -236,6 +238,7 @@ def main():
     by_line = collections.defaultdict(collections.Counter)
     by_fn = collections.defaultdict(collections.Counter)
     prev_cnt = 0.0
+    by_caller = collections.Counter()
     for blk in blocks:
         good, helper = [], []
         info = []
@@ -277,6 +280,12 @@ def main():
             by_mn[mn] += cnt
             by_line[(fl, ln)][kind] += cnt
             by_fn[fn][kind] += cnt
+            if LANE_CALLERS and kind == "lane":
+                k = len(ch) - 1
+                while k >= 0 and ch[k].name and HELPER.search(ch[k].name):
+                    k -= 1
+                site = (ch[k + 1].call_file, ch[k + 1].call_line) if k + 1 < len(ch) else (fl, ln)
+                by_caller[site] += cnt
     tot = sum(kinds.values())
     print(f"estimated per op: total {tot / ops:.1f}  " + "  ".join(f"{k} {v / ops:.1f}" for k, v in kinds.items()))
     print("\nby mnemonic, per op:")
@@ -285,6 +294,10 @@ def main():
     print("\nby function (innermost inlined instance), per op:")
     for fn, c in sorted(by_fn.items(), key=lambda kv: -sum(kv[1].values()))[:top]:
         print(f"  {sum(c.values()) / ops:7.2f}  salu {c['salu'] / ops:6.2f}  valu {c['valu'] / ops:6.2f}  lane {c['lane'] / ops:5.2f}  br {c['branch'] / ops:5.2f}  {fn[:90]}")
+    if LANE_CALLERS:
+        print("\ncontext lane reads/writes by requesting line, per op:")
+        for (fl, ln), c in by_caller.most_common(top):
+            print(f"  {c / ops:7.2f}  {fl}:{ln}")
     print("\nby source line, per op:")
     for (fl, ln), c in sorted(by_line.items(), key=lambda kv: -sum(kv[1].values()))[:top]:
         print(f"  {sum(c.values()) / ops:7.2f}  salu {c['salu'] / ops:6.2f}  valu {c['valu'] / ops:6.2f}  lane {c['lane'] / ops:5.2f}  br {c['branch'] / ops:5.2f}  {fl}:{ln}")

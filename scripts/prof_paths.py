@@ -12,9 +12,12 @@ import crdt_amd  # noqa: E402
 from crdt_amd.traces import load_remote_wire, load_trace  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-local = len(sys.argv) > 2 and sys.argv[2] == "local"
+mode = sys.argv[2] if len(sys.argv) > 2 else "remote"
+local = mode == "local"
 e = crdt_amd.Engine(n, 32)
-if local:
+if mode == "random":  # config 4: 20,000 generated ops per document (bench_config4.py's shape)
+    e.stage_random(list(range(n)), "gen", 20000, 0xC0FFEE)
+elif local:
     t = load_trace("automerge-paper")
     ag = e.agent_intern(list(range(n)), ["jeremy"] * n)
     e.apply_trace(list(range(n)), int(ag[0]), t.counts, t.patches, stage_only=True)
@@ -32,7 +35,7 @@ for m, lab in enumerate(["cycles", "calls", "txns"]):
     s = np.array([e.debug_state(d) for d in range(m, n, 4 * max(1, n // 256))]).astype(np.float64)
     view[lab] = s[:, P0:P0 + 4].mean(axis=0)
 tot = view["cycles"].sum()
-print(f"docs {n} {'local' if local else 'remote'} replay_ms {e.timings()[0]:.1f}")
+print(f"docs {n} {mode} replay_ms {e.timings()[0]:.1f}")
 for i, k in enumerate(names):
     c, calls, tx = view["cycles"][i], view["calls"][i], view["txns"][i]
     print(f"  {k:8s} cycles {c:.4g} ({c / tot:.1%})  calls {calls:.0f}  txns {tx:.0f}  cycles/call {c / max(calls, 1):.0f}  cycles/txn {c / max(tx, 1):.0f}")

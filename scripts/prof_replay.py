@@ -61,6 +61,15 @@ if a.clean:
     hip.hipEventElapsedTime(C.byref(ms), ev[0], ev[1])
     replay_ms = ms.value  # the clean launch, HIP events on the engine stream (as bench.py)
     st = e.status()
-e.publish_async()
-e.sync()
-print("status ok:", bool((st == 0).all()), "replay_ms", replay_ms, "wall", time.time() - t0)
+pub_ms = None
+if a.clean:
+    hip.hipEventRecord(ev[0], s_)
+    e.publish_async()
+    hip.hipEventRecord(ev[1], s_)
+    e.sync()
+    hip.hipEventElapsedTime(C.byref(ms), ev[0], ev[1])
+    pub_ms = ms.value  # publish (k_publish + k_pub_index) of the clean replay, HIP events
+else:
+    e.publish_async()
+    e.sync()
+print("status ok:", bool((st == 0).all()), "replay_ms", replay_ms, "pub_ms", pub_ms, "wall", time.time() - t0)

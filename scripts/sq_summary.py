@@ -17,7 +17,7 @@ ops_doc = int(sys.argv[3]) if len(sys.argv) > 3 else 259778
 tag = sys.argv[4] if len(sys.argv) > 4 else ""
 agg, meta = {}, {}
 for f in sorted(glob.glob(f"gpurun_out/pmc[123]{tag}/**/*counter_collection.csv", recursive=True)):
-    rows = [r for r in csv.DictReader(open(f)) if "k_replay" in r.get("Kernel_Name", "")]
+    rows = [r for r in csv.DictReader(open(f)) if os.environ.get("SQ_KERNEL", "k_replay") in r.get("Kernel_Name", "")]
     last = max(int(r["Dispatch_Id"]) for r in rows)
     for r in rows:
         if int(r["Dispatch_Id"]) == last:
@@ -31,7 +31,7 @@ total_inst = sum(agg.get(k, 0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_I
                                          "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH", "SQ_INSTS_FLAT"))
 wc = agg.get("SQ_WAVE_CYCLES", 0)
 res = {
-    "kernel": "k_replay<32>", "docs": docs, "ops_per_doc": ops_doc, "workload": os.environ.get("SQ_WORKLOAD", "config 2: automerge-paper remote, one clean launch"),
+    "kernel": os.environ.get("SQ_KERNEL", "k_replay") + "<32>", "docs": docs, "ops_per_doc": ops_doc, "workload": os.environ.get("SQ_WORKLOAD", "config 2: automerge-paper remote, one clean launch"),
     "launch": meta, "counters": agg,
     "per_op": {k.replace("SQ_INSTS_", "").lower(): v / ops for k, v in inst.items()},
     "instructions_per_op": total_inst / ops,
