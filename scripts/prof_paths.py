@@ -24,6 +24,7 @@ elif local:
 else:
     e.stage_remote_replicated(load_remote_wire("automerge-paper"), 0, ["u%05d" % i for i in range(n)])
 e.run()
+e.fit()  # (as bench.py / prof_replay.py: capacities = the stream's use, then one clean launch)
 e.reset_async()
 e.run_async()
 e.sync()
@@ -40,4 +41,7 @@ for i, k in enumerate(names):
     c, calls, tx = view["cycles"][i], view["calls"][i], view["txns"][i]
     print(f"  {k:8s} cycles {c:.4g} ({c / tot:.1%})  calls {calls:.0f}  txns {tx:.0f}  cycles/call {c / max(calls, 1):.0f}  cycles/txn {c / max(tx, 1):.0f}")
 s = np.array([e.debug_state(d) for d in range(3, n, 4 * max(1, n // 256))]).astype(np.float64)[:, P0:P0 + 4].mean(axis=0)
-print(f"  delete-call cycles by part: run detection {s[0]:.4g}, first segment {s[1]:.4g}, leaf-split loop {s[2]:.4g}, tail {s[3]:.4g}")
+if mode == "random":
+    print(f"  generated-op cycles by part: draw + op {s[0]:.4g}, fast path without cursor {s[1]:.4g}, cursor in leaf {s[2]:.4g}, leaf switch (commit + descent + load) {s[3]:.4g}")
+else:
+  print(f"  delete-call cycles by part: run detection {s[0]:.4g}, first segment {s[1]:.4g}, leaf-split loop {s[2]:.4g}, tail {s[3]:.4g}")

@@ -115,6 +115,8 @@ struct Replayer {
 #ifdef CRDT_PROF
   u32 prof_cat = 0;  // diagnostic: which fast path ran (0 typing, 2 delete, 3 insert)
   u32 prof_mode = 0; // document d % 4: 0 cycles, 1 calls, 2 txns per path, 3 detail (below)
+  u32 prof_gen = 0;  // generated ops (config 4): detail = gen / fast path / cursor / leaf switch
+  u32 prof_cur = 0, prof_sw = 0;  // cycles in cursor_at_content_pos and in its leaf switches
 #endif
 
   // ------------------------------------------------------------------ context access
@@ -496,18 +498,30 @@ struct Replayer {
   CRDT_HD Cursor cursor_at_start() const { return Cursor{leaf_at_start(), 0, 0}; }  // root.rs:133-150
   // root.rs:54-88 + 401-411, leaf.rs:61-84 (stick_end = false)
   CRDT_HD bool cursor_at_content_pos(u32 pos, Cursor& c) {
+#ifdef CRDT_PROF
+    u64 pc0 = w.clock();
+#endif
     u32 vs = g(C_VSTART);
     if (!(g(C_LEAF) != INVALID && g(C_VS_OK) && pos >= vs && pos < vs + g(C_NOW))) {
+#ifdef CRDT_PROF
+      u64 ps0 = w.clock();
+#endif
       commit();
       u32 lf, blk, i;
       if (!find_by_pos(pos, lf, vs, blk, i)) return false;
       if (lf != g(C_LEAF)) load_cache(lf, (blk << 6) | i, w.ld_raw(w.template at<2>(sol(), lf) + 1));  // (successor: in flight with the entries)
       p(C_VSTART, vs);
       p(C_VS_OK, 1);
+#ifdef CRDT_PROF
+      prof_sw += (u32)(w.clock() - ps0);
+#endif
     }
     u32 idx, off;
     if (!w.cfind_content(g(C_N), pos - vs, idx, off)) return false;
     c = Cursor{g(C_LEAF), idx, off};
+#ifdef CRDT_PROF
+    prof_cur += (u32)(w.clock() - pc0);
+#endif
     return true;
   }
   // doc.rs:101-136 (marker_at + cursor_before_item, leaf.rs:41-57).  `load`: move the cache to
@@ -1655,7 +1669,7 @@ struct Replayer {
     }
     fast_txn_commit(first, done * l);  // (delete orders name no item: no order -> leaf entries)
 #ifdef CRDT_PROF
-    if (prof_mode == 3u) {
+    if (prof_mode == 3u && !prof_gen) {
       inc(S_PROF0, (u32)(pt1 - pt0)); inc(S_PROF1, (u32)(pt2 - pt1));
       inc(S_PROF2, (u32)(pt3 - pt2)); inc(S_PROF3, (u32)(w.clock() - pt3));
     }
@@ -2017,6 +2031,9 @@ struct Replayer {
       agent = h.w1;
       u32 lp = o.w1, del = o.w2;
       ins = o.w3 != 0u;
+#ifdef CRDT_PROF
+      prof_cat = ins ? 3u : 2u;
+#endif
       l = del + o.w3;
       if ((del != 0u) == ins) return 0;
       if (l - 1u >= 0xFFFFu) return 0;
@@ -2215,10 +2232,31 @@ struct Replayer {
             base = done;
             w.gen_draws(h.w3, base);
           }
+#ifdef CRDT_PROF
+          u64 pg0 = w.clock();
+#endif
           Rec d = w.rec_get(done - base);
           Rec go = gen_op_of(d.w0, d.w1, d.w2, cur_len());
           Rec gh{(REC_LTXN << 28) | 1u, h.w1, go.w2, go.w2 + go.w3};
+#ifdef CRDT_PROF
+          u64 pg1 = w.clock();
+          prof_gen = 1u; prof_cur = 0u; prof_sw = 0u;
+          u32 okg = fast_txn(pos, REC_LTXN, 1u, gh, go);
+          prof_gen = 0u;
+          if (prof_mode == 3u && okg) {
+            u32 ft = (u32)(w.clock() - pg1);
+            inc(S_PROF0, (u32)(pg1 - pg0)); inc(S_PROF1, ft - prof_cur);
+            inc(S_PROF2, prof_cur - prof_sw); inc(S_PROF3, prof_sw);
+          } else if (okg) {  // modes 0-2: cycles / calls / txns of the fast path by kind (typing, delete, insert)
+            u32 dt = prof_mode == 0u ? (u32)(w.clock() - pg1) : 1u;
+            if (prof_cat == 0u) inc(S_PROF0, dt);
+            else if (prof_cat == 2u) inc(S_PROF2, dt);
+            else inc(S_PROF3, dt);
+          }
+          if (!okg) break;
+#else
           if (!fast_txn(pos, REC_LTXN, 1u, gh, go)) break;
+#endif
           done++;
         }
         p(S_GEN_DONE, done);
