@@ -502,7 +502,9 @@ struct Replayer {
     u64 pc0 = w.clock();
 #endif
     u32 vs = g(C_VSTART);
-    if (!(g(C_LEAF) != INVALID && g(C_VS_OK) && pos >= vs && pos < vs + g(C_NOW))) {
+    // (C_VS_OK implies a cached leaf: it is 0 from begin() until a descent or a leaf start sets
+    // it; pos in [vs, vs + now) is one unsigned compare)
+    if (!(g(C_VS_OK) && pos - vs < g(C_NOW))) {
 #ifdef CRDT_PROF
       u64 ps0 = w.clock();
 #endif
@@ -1344,10 +1346,13 @@ struct Replayer {
   // Conditions are written as early exits throughout the fast paths: each is one s_cmp and one
   // branch, where an `a & b & ...` chain of uniform compares becomes 64-bit lane masks (s_cmp,
   // s_cselect_b64, s_and_b64 per term) on the scalar unit this kernel is bound by.
-  CRDT_HD u32 fast_txn_ok(u32 agent, u32 seq, u32 first) const {
+  // (local: seq is the author's next seq by definition (doc.rs:393-398), so that check is skipped)
+  CRDT_HD u32 fast_txn_ok(u32 agent, u32 seq, u32 first, u32 local = 0u) const {
     if (agent != g(T_AG_ID)) return 0;
     u32 ll = g(T_AGL_LEN);
-    if (seq != g(T_AGL_KEY) + ll) return 0;
+    if (!local) {
+      if (seq != g(T_AGL_KEY) + ll) return 0;
+    }
     if (g(F_FAST)) return 1;
     if (g(T_AG_CNT) == 0u) return 0;
     if (g(T_AGL_ORDER) + ll != first) return 0;
@@ -2035,13 +2040,15 @@ struct Replayer {
       prof_cat = ins ? 3u : 2u;
 #endif
       l = del + o.w3;
-      if ((del != 0u) == ins) return 0;
-      if (l - 1u >= 0xFFFFu) return 0;
+      if (!gen) {  // (a generated op is one insert of 1 char or one delete of 1..10: well-formed by construction)
+        if ((del != 0u) == ins) return 0;
+        if (l - 1u >= 0xFFFFu) return 0;
+      }
       if (gen_form) {
         u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l);
         if (!ok) return 0;
       }
-      if (!fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first)) return 0;
+      if (!fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first, 1u)) return 0;
       if (ins && lp == 0u) {
         // doc.rs:443-444: origin_left ROOT, the cursor at the start of the document (root.rs:133-
         // 150); integrate stops at once (origin_right is the item there) and insert_internal puts
