@@ -27,6 +27,7 @@ constexpr u32 ROOT_ORDER = 0xFFFFFFFFu;   // list/mod.rs:30
 constexpr u32 ROOT_AGENT = 0xFFFFu;       // "ROOT" -> AgentId::MAX (doc.rs:68)
 constexpr u32 UNKNOWN_AGENT = 0xFFFEu;    // a name that is not (yet) interned for this document
 constexpr u32 INVALID = 0xFFFFFFFFu;
+constexpr u32 VS_BAD = 0x80000000u;       // the cached leaf's visible start is unknown (no position is in range)
 
 constexpr u32 GROUP = 64;                 // directory slots per block (one wavefront)
 // Root level of the directory: one group (block id, slot count, visible count) per directory

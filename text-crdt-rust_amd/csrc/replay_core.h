@@ -77,7 +77,7 @@ enum : u32 {
   // tail, which the fast path reads); materialize_tails() brings them up to date.
   F_BASE,
   // x2: leaf cache bookkeeping
-  C_LEAF = 128, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK,
+  C_LEAF = 128, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK /* (unused) */,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order (INVALID: not known)
   // RLE tails
   T_CWO_KEY, T_CWO_AGENT, T_CWO_SEQ, T_CWO_LEN,
@@ -193,13 +193,12 @@ struct Replayer {
     p(C_NOW, 0);
     p(C_BLK, 0);
     p(C_I, 0);
-    p(C_VSTART, 0);
+    p(C_VSTART, VS_BAD);
     p(C_DIRTY, 0);
-    p(C_VS_OK, 0);
     p(C_SUCC, INVALID);
     p(C_SUCC_ORD, 0);
     p(T_CWO_KEY, 0); p(T_CWO_AGENT, 0); p(T_CWO_SEQ, 0); p(T_CWO_LEN, 0);
-    p(T_DEL_KEY, 0); p(T_DEL_ORDER, 0); p(T_DEL_LEN, 0);
+    p(T_DEL_KEY, INVALID); p(T_DEL_ORDER, 0); p(T_DEL_LEN, 0);  // (no run: no key continues it)
     p(T_TX_ORDER, 0); p(T_TX_LEN, 0); p(T_TX_SHADOW, 0);
     p(T_FR0, ROOT_ORDER);
     p(T_AG_ID, INVALID); p(T_AG_BASE, 0); p(T_AG_CNT, 0); p(T_AG_CAP, 0);
@@ -387,7 +386,7 @@ struct Replayer {
     u32 v = w.cache_vis_from(0u);
     p(C_NOW, v);
     p(C_VIS, v);
-    p(C_VS_OK, 0);
+    p(C_VSTART, VS_BAD);
     p(C_SUCC, w.uni_(succ));
     p(C_SUCC_ORD, INVALID);
   }
@@ -502,9 +501,9 @@ struct Replayer {
     u64 pc0 = w.clock();
 #endif
     u32 vs = g(C_VSTART);
-    // (C_VS_OK implies a cached leaf: it is 0 from begin() until a descent or a leaf start sets
-    // it; pos in [vs, vs + now) is one unsigned compare)
-    if (!(g(C_VS_OK) && pos - vs < g(C_NOW))) {
+    // (pos in [vs, vs + now) is one unsigned compare; an unknown start is VS_BAD, which no
+    // position passes, and there is no cached leaf only while it is VS_BAD)
+    if (!(pos - vs < g(C_NOW))) {
 #ifdef CRDT_PROF
       u64 ps0 = w.clock();
 #endif
@@ -513,7 +512,6 @@ struct Replayer {
       if (!find_by_pos(pos, lf, vs, blk, i)) return false;
       if (lf != g(C_LEAF)) load_cache(lf, (blk << 6) | i, w.ld_raw(w.template at<2>(sol(), lf) + 1));  // (successor: in flight with the entries)
       p(C_VSTART, vs);
-      p(C_VS_OK, 1);
 #ifdef CRDT_PROF
       prof_sw += (u32)(w.clock() - ps0);
 #endif
@@ -694,7 +692,7 @@ struct Replayer {
         w.cache_from_moved();
         u32 v = w.cache_vis_from(0u);
         p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
-        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 0); p(C_VS_OK, 0);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 0); p(C_VSTART, VS_BAD);
         p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
         p(C_N, space + moved);
         c.leaf = nl;
@@ -828,12 +826,10 @@ struct Replayer {
   CRDT_HD void append_delete(u32 key, u32 target, u32 len) {  // Rle<KVPair<DeleteEntry>>::append
     u32 n = g(S_N_DEL);
     u32 dk = g(T_DEL_KEY), dlen = g(T_DEL_LEN);
-    if (n != 0u) {
-      if (key == dk + dlen) {
-        if (g(T_DEL_ORDER) + dlen == target) {
-          p(T_DEL_LEN, dlen + len);
-          return;
-        }
+    if (key == dk + dlen) {  // (with no run yet dk + dlen is INVALID, which no key equals)
+      if (g(T_DEL_ORDER) + dlen == target) {
+        p(T_DEL_LEN, dlen + len);
+        return;
       }
     }
     if (n) w.st(&w.at(dels(), n - 1)->len, dlen);
@@ -1768,7 +1764,7 @@ struct Replayer {
         w.cache_from_moved();
         u32 v = w.cache_vis_from(0u);
         p(C_LEAF, nl); p(C_BLK, nblk); p(C_I, ni);
-        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 1u); p(C_VS_OK, 0);
+        p(C_NOW, v); p(C_VIS, v); p(C_DIRTY, 1u); p(C_VSTART, VS_BAD);
         p(C_SUCC, succ); p(C_SUCC_ORD, succ_ord);
         p(C_N, m + moved);
         leaf = nl;
@@ -1962,7 +1958,9 @@ struct Replayer {
     u32 remote = ((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u;
     u32 per = per_txn(remote);
     u32 rn = rec_n();
-    if (g(C_LEAF) == INVALID) return 0;
+    if (!gen) {  // (the GEN loop is entered with a cached leaf, which the fast paths never drop)
+      if (g(C_LEAF) == INVALID) return 0;
+    }
     u32 b0 = 0, nv = 0;
     Rec h = gh, o = go, pr{0, 0, 0, 0};
     if (!gen) {
@@ -2048,7 +2046,9 @@ struct Replayer {
         u32 ok = (h.w0 == ((REC_LTXN << 28) | 1u)) & (o.w0 == (REC_LOP << 28)) & (h.w2 == del) & (h.w3 == l);
         if (!ok) return 0;
       }
-      if (!fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first, 1u)) return 0;
+      if (!gen) {  // (the GEN loop checks it once on entry: its fast commits keep it true)
+        if (!fast_txn_ok(agent, g(T_AGL_KEY) + g(T_AGL_LEN), first, 1u)) return 0;
+      }
       if (ins && lp == 0u) {
         // doc.rs:443-444: origin_left ROOT, the cursor at the start of the document (root.rs:133-
         // 150); integrate stops at once (origin_right is the item there) and insert_internal puts
@@ -2056,7 +2056,6 @@ struct Replayer {
         c = cursor_at_start();
         ensure(c.leaf);
         p(C_VSTART, 0u);  // (the first leaf starts at visible position 0)
-        p(C_VS_OK, 1u);
         ol = ROOT_ORDER;
       } else {
         if (!cursor_at_content_pos(ins ? lp - 1u : lp, c)) return 0;  // root.rs:54-88 (loads the leaf)
@@ -2234,6 +2233,10 @@ struct Replayer {
         p(T_RB_BASE, 0x80000000u);
         u32 base = done;
         w.gen_draws(h.w3, base);
+        // The general path goes first while there is no cached leaf yet, or while the fast-commit
+        // conditions (fast_txn_ok) do not hold; once they do, every fast commit keeps them (the
+        // author stays cached and its tails extend), so the generated ops skip the check
+        if (g(C_LEAF) == INVALID || !fast_txn_ok(h.w1, g(T_AGL_KEY) + g(T_AGL_LEN), g(S_NEXT_ORDER), 1u)) n_gen = done;
         while (done < n_gen) {
           if (done - base >= 64u) {
             base = done;
