@@ -226,7 +226,7 @@ struct Replayer {
     p(S_LEN, 0);
     p(S_N_CWO, 0); p(S_N_DEL, 0); p(S_N_DD, 0); p(S_N_TXN, 0); p(S_N_PAR, 0);
     p(S_N_FR, 1);
-    p(S_N_ITEMS, 0);
+    p(S_N_ITEMS, 0);  // (not maintained: no reader)
     p(S_CAP_NEED, 0);
     p(S_N_ENTRIES, 0);
     p(S_GEN_DONE, 0);
@@ -1246,7 +1246,6 @@ struct Replayer {
         if (scanning) c = scan_start;
         a0 = item;
         n = 1;
-        inc(S_N_ITEMS, (u32)item.len);
         mode = M_FETCH;
       } else {
         if (mode == M_LDEL) {  // mutations.rs:541-556 local_deactivate
@@ -1422,7 +1421,6 @@ struct Replayer {
     w.cset(idx, e);  // (e is visible: the count grows by total)
     p(C_NOW, g(C_NOW) + total);
     p(C_DIRTY, 1u);
-    inc(S_N_ITEMS, total);
     fast_txn_commit(first, total);
     return nt * per_txn(remote);
   }
@@ -1815,7 +1813,6 @@ struct Replayer {
     w.cset(idx + 1u, item);
     p(C_NOW, g(C_NOW) + len);
     p(C_DIRTY, 1u);
-    inc(S_N_ITEMS, len);
     return 1;
   }
   // The item as entry 0 of the cached first leaf (cursor at the start of the document, offset 0 at
@@ -1847,7 +1844,6 @@ struct Replayer {
     });
     p(C_NOW, g(C_NOW) + m * len);
     p(C_DIRTY, 1u);
-    inc(S_N_ITEMS, m * len);
     return m;
   }
   // A local delete of l visible items that starts at offset `off` of visible entry idx of the
@@ -2095,7 +2091,6 @@ struct Replayer {
         // the item, splitting the leaf (mutations.rs:17-179): do that here when a leaf is free
         if ((g(K_LEAF) - g(S_N_LEAVES) >= 2u) && (g(K_MAP) - first >= l)) {
           insert_items(item, Span{0, 0, 0, 0}, Span{0, 0, 0, 0}, 1u, c, INVALID);
-          inc(S_N_ITEMS, l);
           fast_txn_commit(first, l);
           return per;
         }
