@@ -1794,8 +1794,7 @@ struct Replayer {
     u32 n = g(C_N);
     u32 len = (u32)item.len;
     u32 has_rem = off < slen(e);
-    u32 space = 1u + has_rem;
-    if (n + space > (u32)L) return 0;
+    u32 space = 1u + has_rem;  // (fits: the caller sent n + space > L to the split path)
     if (g(K_MAP) - item.order < len) return 0;
     // entry writes straight to the cache (truncating e keeps its visible items in e + rem); the
     // visible count grows by exactly the item's len
@@ -2114,7 +2113,9 @@ struct Replayer {
     }
     i32 el = w.cget_len(idx);
     if (el <= 0) return 0;                // already deleted
-    if (c.off + l > (u32)el) return 0;    // spans entries
+    if (remote) {  // (a local delete that spans entries went to leaf_delete_span above)
+      if (c.off + l > (u32)el) return 0;  // spans entries
+    }
 #ifdef CRDT_PROF
     prof_cat = 2u;
 #endif
