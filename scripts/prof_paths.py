@@ -43,5 +43,8 @@ for i, k in enumerate(names):
 s = np.array([e.debug_state(d) for d in range(3, n, 4 * max(1, n // 256))]).astype(np.float64)[:, P0:P0 + 4].mean(axis=0)
 if mode == "random":
     print(f"  generated-op cycles by part: draw + op {s[0]:.4g}, fast path without cursor {s[1]:.4g}, cursor in leaf {s[2]:.4g}, leaf switch (commit + descent + load) {s[3]:.4g}")
+elif os.environ.get("PROF_LOOP"):  # a -DCRDT_PROF_LOOP build: detail of the leaf-split loop
+    print(f"  leaf-split loop cycles by part: delete_general without split_at {s[0]:.4g}, split_at {s[1]:.4g}, "
+          f"find_order + checks {s[2]:.4g}, delete_segment {s[3]:.4g}")
 else:
-  print(f"  delete-call cycles by part: run detection {s[0]:.4g}, first segment {s[1]:.4g}, leaf-split loop {s[2]:.4g}, tail {s[3]:.4g}")
+    print(f"  delete-call cycles by part: run detection {s[0]:.4g}, first segment {s[1]:.4g}, leaf-split loop {s[2]:.4g}, tail {s[3]:.4g}")

@@ -334,6 +334,7 @@ struct WaveCPU {
   void root_add_vis(u32 g, u32 d) { gv[g] += d; }
   void root_add_vis_blk(u32 ng, u32 blk, u32 d) { root_add_vis(root_find_blk(ng, blk), d); }
   void root_set(u32 g, u32 blk, u32 cnt, u32 vis) { gb[g] = blk; gc[g] = cnt; gv[g] = vis; }
+  void root_set_cnt(u32 g, u32 cnt) { gc[g] = cnt; }
   void root_insert(u32 ng, u32 g, u32 blk, u32 cnt, u32 vis) {
     root_room(ng + 2);
     for (u32 i = ng; i > g; i--) { gb[i] = gb[i - 1]; gc[i] = gc[i - 1]; gv[i] = gv[i - 1]; }
@@ -370,17 +371,22 @@ struct WaveCPU {
   // checks against the row's current contents: the early-requested rows must still be current)
   static u32 row_digest(const u32* p) { u32 h = 2166136261u; for (u32 k = 0; k < 64; k++) h = (h ^ p[k]) * 16777619u; return h; }
   u32 row_ld(const u32* p) const { return row_digest(p); }
-  void blk_insert(u32 ol, u32 ov, u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+  static void row_check(u32 ol, u32 ov, const u32* dl, const u32* dv) {
     if (ol != row_digest(dl) || ov != row_digest(dv)) {
-      std::fprintf(stderr, "wave_cpu: directory row changed between row_ld and blk_insert\n");
+      std::fprintf(stderr, "wave_cpu: directory row changed between row_ld and its use\n");
       std::abort();
     }
-    for (u32 k = cnt; k > i; k--) { dl[k] = dl[k - 1]; dv[k] = dv[k - 1]; }
-    dl[i] = leaf;
-    dv[i] = vis;
-    for (u32 k = i; k <= cnt; k++) sol[2 * dl[k]] = (blk << 6) | k;  // ({slot, successor} entries)
   }
-  u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
+  void blk_insert_at(u32 ol, u32 ov, u32* dl, u32* dv, u32 cnt, u32 i, u32 vis_i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+    row_check(ol, ov, dl, dv);
+    dv[i] = vis_i;
+    for (u32 k = cnt; k > i + 1; k--) { dl[k] = dl[k - 1]; dv[k] = dv[k - 1]; }
+    dl[i + 1] = leaf;
+    dv[i + 1] = vis;
+    for (u32 k = i + 1; k <= cnt; k++) sol[2 * dl[k]] = (blk << 6) | k;  // ({slot, successor} entries)
+  }
+  u32 blk_split_r(u32 rl, u32 rv, const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
+    row_check(rl, rv, dl, dv);
     u32 t = 0;
     for (u32 k = 32; k < 64; k++) {
       ndl[k - 32] = dl[k];
@@ -390,6 +396,8 @@ struct WaveCPU {
     }
     return t;
   }
+  // (the GPU shifts the rows it holds; here the new block's rows as blk_split_r wrote them)
+  void rows_upper(u32& rl, u32& rv, const u32* ndl, const u32* ndv) const { rl = row_digest(ndl); rv = row_digest(ndv); }
 };
 
 }  // namespace crdt

@@ -22,6 +22,11 @@ typedef uint64_t u64;
 typedef int64_t i64;
 
 #define CRDT_HD __host__ __device__ __forceinline__
+// Event counters of the CPU emulation's statistics build (tests/emu stats: path counts for the
+// design notes); nothing in the product builds.
+#ifndef CRDT_STAT
+#define CRDT_STAT(k, v) ((void)0)
+#endif
 
 constexpr u32 ROOT_ORDER = 0xFFFFFFFFu;   // list/mod.rs:30
 constexpr u32 ROOT_AGENT = 0xFFFFu;       // "ROOT" -> AgentId::MAX (doc.rs:68)

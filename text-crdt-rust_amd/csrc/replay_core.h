@@ -117,6 +117,7 @@ struct Replayer {
   u32 prof_mode = 0; // document d % 4: 0 cycles, 1 calls, 2 txns per path, 3 detail (below)
   u32 prof_gen = 0;  // generated ops (config 4): detail = gen / fast path / cursor / leaf switch
   u32 prof_cur = 0, prof_sw = 0;  // cycles in cursor_at_content_pos and in its leaf switches
+  u32 prof_split = 0;  // cycles in split_at (-DCRDT_PROF_LOOP: detail of fast_deletes' leaf-split loop)
 #endif
 
   // ------------------------------------------------------------------ context access
@@ -579,8 +580,16 @@ struct Replayer {
   // extra_vis: visible items the caller puts into the new leaf's padding slots in HBM itself
   // (counted in its directory slot, its group and the document length here)
   CRDT_HD u32 split_at(u32 idx, u32 padding, u32 extra_vis = 0u) {
+#ifdef CRDT_PROF
+    u64 psa = w.clock();
+#endif
+    u32 blk = g(C_BLK), i = g(C_I);
+    // the cached leaf's directory block rows (blk_insert_at shifts them), requested first: their
+    // latency overlaps the successor, leaf and order-map writes below
+    u32 rl = w.row_ld(dleaf(blk)), rv = w.row_ld(dvis(blk));
     u32 nl = g(S_N_LEAVES);
     p(S_N_LEAVES, nl + 1);
+    CRDT_STAT(0, 1); CRDT_STAT(1, g(C_N) - idx); CRDT_STAT(16 + idx, 1);
     // the leaf list: nl goes right after the cached leaf
     u32 osucc = cached_succ_leaf();
     w.st(w.template at<2>(sol(), nl) + 1, osucc == INVALID ? END_LEAF : osucc);
@@ -595,29 +604,37 @@ struct Replayer {
     p(C_N, idx);
     p(C_DIRTY, 1u);
     // link nl right after the cached leaf (directory block insert; the block splits when full)
-    u32 blk = g(C_BLK), i = g(C_I);
     u32 ng = g(S_NG);
     u32 gg = w.root_find_blk(ng, blk);
     u32 cnt = w.root_cnt(gg);
     if (cnt == GROUP) {  // split the block: [32, 64) -> new block in group gg+1
       u32 nb = g(S_N_BLOCKS);
       p(S_N_BLOCKS, nb + 1);
-      u32 mv = w.blk_split(dleaf(blk), dvis(blk), dleaf(nb), dvis(nb), sol(), nb);
+      u32 mv = w.blk_split_r(rl, rv, dleaf(blk), dvis(blk), dleaf(nb), dvis(nb), sol(), nb);
       w.root_set(gg, blk, 32u, w.root_vis(gg) - mv);
       w.root_insert(ng, gg + 1, nb, 32u, mv);
       p(S_NG, ng + 1);
-      if (i >= 32) { blk = nb; i -= 32; gg = gg + 1; p(C_BLK, nb); p(C_I, i); }
+      if (i >= 32) {
+        w.rows_upper(rl, rv, dleaf(nb), dvis(nb));
+        blk = nb; i -= 32; gg = gg + 1; p(C_BLK, nb); p(C_I, i);
+      }
       cnt = 32;
     }
-    w.blk_insert(w.row_ld(dleaf(blk)), w.row_ld(dvis(blk)), dleaf(blk), dvis(blk), cnt, i + 1, nl, stolen + extra_vis, sol(), blk);
-    // the cached leaf's directory count loses `stolen` (moved to nl); group total unchanged
-    w.root_set(gg, blk, cnt + 1, w.root_vis(gg) + extra_vis);
-    if (extra_vis) inc(S_LEN, extra_vis);
+    // the cached leaf's slot loses `stolen` (moved to nl, the next slot); the group's visible
+    // total changes only by extra_vis
     u32 cv = g(C_VIS) - stolen;
-    w.st(dvis(blk) + i, cv);
+    w.blk_insert_at(rl, rv, dleaf(blk), dvis(blk), cnt, i, cv, nl, stolen + extra_vis, sol(), blk);
+    w.root_set_cnt(gg, cnt + 1u);
+    if (extra_vis) {
+      w.root_add_vis(gg, extra_vis);
+      inc(S_LEN, extra_vis);
+    }
     p(C_VIS, cv);
     p(C_SUCC, nl);
     p(C_SUCC_ORD, padding ? INVALID : first_moved);  // (padding: the caller writes nl's first entries)
+#ifdef CRDT_PROF
+    prof_split += (u32)(w.clock() - psa);
+#endif
     return nl;
   }
   // mutations.rs:17-179 insert_internal.  Items a0..a(n-1) (n <= 3) stay in named registers;
@@ -675,6 +692,7 @@ struct Replayer {
     bool rem_moved = false;
     u32 cn = g(C_N);
     if (cn + space > (u32)L) {
+      CRDT_STAT(8, 1);
       bool follow = c.idx >= (u32)L / 2;
       u32 moved = cn - c.idx;
       u32 succ = g(C_SUCC), succ_ord = g(C_SUCC_ORD);  // the old leaf's successor follows nl
@@ -1629,7 +1647,15 @@ struct Replayer {
     // The leaf ran out of room (or the run reached a shape the segment does not take): the next
     // delete goes the general way -- mutate_entry + insert_internal, splitting the leaf -- and the
     // rest of the run continues from wherever its next target now lives.
+    CRDT_STAT(9, 1); CRDT_STAT(12, k); CRDT_STAT(13, split_first);
+#ifdef CRDT_PROF_LOOP
+    u32 lp_gen = 0, lp_split = 0, lp_find = 0, lp_seg = 0;
+#endif
     while (done < k) {
+#ifdef CRDT_PROF_LOOP
+      u64 q0 = w.clock();
+#endif
+      CRDT_STAT(10, 1);
       if (g(K_LEAF) - g(S_N_LEAVES) < 2u) break;
       Cursor c{g(C_LEAF), idx, off};
       if (done != 0u) {
@@ -1638,7 +1664,18 @@ struct Replayer {
       i32 el = w.cget_len(c.idx);
       if (el <= 0) break;
       if (c.off + l > (u32)el) break;
+      CRDT_STAT(back ? 48 : 49, 1); CRDT_STAT(52, c.off == 0u);
+#ifdef CRDT_PROF_LOOP
+      u64 q1 = w.clock();
+      prof_split = 0;
+#endif
       delete_general(c.idx, c.off, l, back);
+#ifdef CRDT_PROF_LOOP
+      u64 q2 = w.clock();
+      lp_gen += (u32)(q2 - q1) - prof_split;
+      lp_split += prof_split;
+      lp_find += (u32)(q1 - q0);
+#endif
       done++;
       if (done == k) break;
       u32 t2 = back ? t1 - done : t1 + done;
@@ -1646,7 +1683,16 @@ struct Replayer {
       el = w.cget_len(c.idx);
       if (el <= 0) break;
       if (c.off + l > (u32)el) break;
-      done += delete_segment(c.idx, c.off, t2, k - done, back, l);
+#ifdef CRDT_PROF_LOOP
+      u64 q3 = w.clock();
+      lp_find += (u32)(q3 - q2);
+#endif
+      u32 dseg = delete_segment(c.idx, c.off, t2, k - done, back, l);
+#ifdef CRDT_PROF_LOOP
+      lp_seg += (u32)(w.clock() - q3);
+#endif
+      CRDT_STAT(53, dseg); CRDT_STAT(54, dseg == 0u);
+      done += dseg;
     }
 #ifdef CRDT_PROF
     u64 pt3 = w.clock();
@@ -1669,8 +1715,13 @@ struct Replayer {
     fast_txn_commit(first, done * l);  // (delete orders name no item: no order -> leaf entries)
 #ifdef CRDT_PROF
     if (prof_mode == 3u && !prof_gen) {
+#ifdef CRDT_PROF_LOOP
+      (void)pt0; (void)pt1; (void)pt2; (void)pt3;
+      inc(S_PROF0, lp_gen); inc(S_PROF1, lp_split); inc(S_PROF2, lp_find); inc(S_PROF3, lp_seg);
+#else
       inc(S_PROF0, (u32)(pt1 - pt0)); inc(S_PROF1, (u32)(pt2 - pt1));
       inc(S_PROF2, (u32)(pt3 - pt2)); inc(S_PROF3, (u32)(w.clock() - pt3));
+#endif
     }
 #endif
     return done * per;
@@ -1679,6 +1730,7 @@ struct Replayer {
   // or op by op, while the leaf has room.  Returns the deletes applied.
   CRDT_HD u32 delete_segment(u32 idx, u32 off, u32 t, u32 k, u32 back, u32 l) {
     u32 done = k >= 2u ? delete_run_closed(idx, off, t, k, back) : 0u;
+    CRDT_STAT(11, done); CRDT_STAT(14, 1);
     if (done == 0u) {  // op by op
       for (u32 j = 0; j < k; j++) {
         u32 ij = back ? idx : (j == 0u ? idx : idx + (off > 0u) + j);  // forward: the remainder moves right
@@ -1702,6 +1754,7 @@ struct Replayer {
   // back: a backspace run goes on at the item before t, in the first part at idx: a split that
   // would move the cache to the new leaf writes the pieces there in HBM and keeps the old leaf.
   CRDT_HD void delete_general(u32 idx, u32 off, u32 l, u32 back) {
+    CRDT_STAT(7, 1);
     Span e = w.cget(idx);
     u32 n = g(C_N);
     u32 t = e.order + off;
@@ -1734,6 +1787,7 @@ struct Replayer {
     p(C_NOW, g(C_NOW) - l - unplaced_vis);
     p(C_DIRTY, 1u);
     (void)pre_vis;
+    CRDT_STAT(50, m == 0u);
     if (m == 0u) return;
     inc(S_N_ENTRIES, m);
     u32 ci = idx + 1u;
@@ -1744,6 +1798,7 @@ struct Replayer {
       u32 follow = ci >= (u32)L / 2u ? 1u : 0u;
       u32 moved = n - ci;
       u32 succ = g(C_SUCC), succ_ord = g(C_SUCC_ORD);  // the old leaf's successor follows nl
+      CRDT_STAT(follow & back ? 4 : follow ? 5 : 6, 1);
       if (follow & back) {  // the pieces lead the new leaf in HBM; the old leaf stays cached
         u32 nl = split_at(ci, m, unplaced_vis);
         Span* q = leafp(nl);
@@ -1771,6 +1826,7 @@ struct Replayer {
         p(C_N, ci + m);
       }
     } else {
+      CRDT_STAT(51, 1);
       w.cache_shift_right(ci, n, m);
       p(C_N, n + m);
     }

@@ -498,7 +498,7 @@ struct WaveGPU {
     for (u32 t = 0; t < T; t += 64) {
       u32 j = t + l;
       u32 m = 0;
-      for (u32 step = 32; step; step >>= 1)
+      for (u32 step = (u32)L / 2u; step; step >>= 1)  // (entries sit in lanes < L: m < L)
         if (shfl(Pi, m + step - 1u) <= j) m += step;
       u32 pm = shfl(Pi, m), lm = shfl(ln, m), om = shfl(eo, m);
       if (j < T) base[om + (j - (pm - lm))] = v;
@@ -976,6 +976,16 @@ struct WaveGPU {
       gob()[blk] = g;
     }
   }
+  // the slot count of group g := cnt (its block, visible count and block -> group entry unchanged)
+  __device__ __forceinline__ void root_set_cnt(u32 g, u32 cnt) {
+    if constexpr (HR) {
+      u32 j, cb, vb;
+      u32 t = hr_locate(g, j, cb, vb);
+      hc(uni(trow()[t]))[j] = cnt;
+    } else {
+      rcnt()[g] = cnt;
+    }
+  }
   // insert a group at index g, shifting [g, ng) up by one: 64-group chunks from the top down, each
   // read completely before it is written (a chunk's lane 0 reads the top of the chunk below,
   // which is written only afterwards).  HR: a 64-lane shift inside the group's row; a full row
@@ -1136,31 +1146,43 @@ struct WaveGPU {
     leaf = rdlane(lf, k);
     return true;
   }
-  // a 64-slot directory row, one slot per lane (requested early by split_at: see blk_insert)
+  // a 64-slot directory row, one slot per lane (requested first by split_at: see blk_insert_at)
   __device__ __forceinline__ u32 row_ld(const u32* p) const { return *(const u32*)(p + lane()); }
-  // insert (leaf, vis) at slot i of a block whose rows ol / ov (row_ld) hold cnt slots
-  __device__ __forceinline__ void blk_insert(u32 ol, u32 ov, u32* dl, u32* dv, u32 cnt, u32 i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
+  // A leaf inserted after slot i of a block whose rows ol / ov (row_ld) hold cnt slots: slot i's
+  // visible count becomes vis_i, (leaf, vis) goes to slot i + 1 and slots [i + 1, cnt) move up one.
+  // One store per row and one slot-table store per moved leaf (lanes [i, cnt]).
+  __device__ __forceinline__ void blk_insert_at(u32 ol, u32 ov, u32* dl, u32* dv, u32 cnt, u32 i, u32 vis_i, u32 leaf, u32 vis,
+                                                u32* sol, u32 blk) const {
     u32 l = lane();
     u32 sl = shfl(ol, l - 1), sv = shfl(ov, l - 1);
-    u32 nlf = l < i ? ol : (l == i ? leaf : sl);
-    u32 nvs = l < i ? ov : (l == i ? vis : sv);
+    u32 j = i + 1u;
+    u32 nlf = l <= i ? ol : (l == j ? leaf : sl);
+    u32 nvs = l < i ? ov : (l == i ? vis_i : (l == j ? vis : sv));
     if (l >= i && l <= cnt) {
       *(u32*)(dl + l) = nlf;
       *(u32*)(dv + l) = nvs;
       *(u32*)(sol + 2u * nlf) = (blk << 6) | l;  // (slot entries are {slot, successor})
     }
   }
-  __device__ __forceinline__ u32 blk_split(const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
+  // slots [32, 64) of a full block (rows rl / rv, row_ld) move to [0, 32) of block nb; returns
+  // their visible total
+  __device__ __forceinline__ u32 blk_split_r(u32 rl, u32 rv, const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol,
+                                             u32 nb) const {
+    (void)dl; (void)dv;
     u32 l = lane();
-    u32 lf = 0, v = 0;
     if (l >= 32) {
-      lf = *(const u32*)(dl + l);
-      v = *(const u32*)(dv + l);
-      *(u32*)(ndl + l - 32) = lf;
-      *(u32*)(ndv + l - 32) = v;
-      *(u32*)(sol + 2u * lf) = (nb << 6) | (l - 32);
+      *(u32*)(ndl + l - 32) = rl;
+      *(u32*)(ndv + l - 32) = rv;
+      *(u32*)(sol + 2u * rl) = (nb << 6) | (l - 32);
     }
-    return wave_sum(v);
+    return wave_sum(l >= 32 ? rv : 0u);
+  }
+  // the rows of the new block after blk_split_r (lanes >= 32 wrap: past its 32 slots)
+  __device__ __forceinline__ void rows_upper(u32& rl, u32& rv, const u32* ndl, const u32* ndv) const {
+    (void)ndl; (void)ndv;
+    u32 s = lane() + 32u;
+    rl = shfl(rl, s);
+    rv = shfl(rv, s);
   }
 };
 
