@@ -229,6 +229,22 @@ def golden_pos_seq(trace: str):
     return np.cumsum(d.astype(np.int64)).astype(np.uint32)
 
 
+def golden_seq_pos(trace: str):
+    """Committed fixture (tests/golden/ap_remote_seq_pos.delta.gz, made by make_queries.py from the
+    oracle): (position, deleted) of every seq of the trace's remote replay (one author, agent 0;
+    Cursor::count_pos, cursor.rs:147-190), or None."""
+    import gzip
+    if trace != "automerge-paper":
+        return None
+    try:
+        b = gzip.open(os.path.join(ROOT, "tests", "golden", "ap_remote_seq_pos.delta.gz")).read()
+    except OSError:
+        return None
+    n = len(b) // 5
+    d = np.frombuffer(b[:4 * n], np.int32)
+    return np.cumsum(d.astype(np.int64)).astype(np.uint32), np.frombuffer(b[4 * n:], np.uint8).copy()
+
+
 TRAFFIC_WORKLOAD = {"k_replay": "automerge-paper remote, one clean launch",
                     "k_materialize": "automerge-paper remote, per-document content copies, one launch"}
 
@@ -502,11 +518,20 @@ def main():
     ok = bool((st == 0).all())
     q_ok = bool(((d_p2 == d_pos) & (d_del == 0) & (d_ag == 0)).all().item()) if q else True
     gseq = golden_pos_seq(args.trace)  # every timed pos -> loc answer against the oracle's (fixture)
-    q_gold = None
+    gpos = golden_seq_pos(args.trace)  # every timed loc -> pos answer against the oracle's (fixture)
+    q_gold = q_gold_loc = None
     if q and gseq is not None and int(lens.min()) == gseq.shape[0] == int(lens.max()):
         g = torch.from_numpy(gseq.view(np.int32)).to(dev)
         q_gold = bool((d_seq == g[d_pos.long()]).all().item())
         q_ok = q_ok and q_gold
+    if q and gpos is not None:
+        gp = torch.from_numpy(gpos[0].view(np.int32)).to(dev)
+        gd = torch.from_numpy(gpos[1]).to(dev)
+        sq = d_seq.long()
+        ix = sq.clamp(0, gp.shape[0] - 1)
+        q_gold_loc = bool(((sq >= 0) & (sq < gp.shape[0])).all().item()) and \
+            bool(((d_p2 == gp[ix]) & (d_del == gd[ix])).all().item())
+        q_ok = q_ok and q_gold_loc
     dg = eng.digests()
     t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, torch.device("cpu") if args.share_gpu else dev)
     gold = golden(args.trace, "remote_digest")
@@ -559,9 +584,11 @@ def main():
             "cpu_baseline": cpu,
             "parity_ok": ok,
             "parity": "every document's digest == committed oracle golden digest (tests/golden); every timed "
-                      "pos->loc answer == the oracle's (tests/golden/ap_remote_pos_seq.delta.gz) and round-trips "
-                      "through loc->pos",
+                      "pos->loc answer == the oracle's (tests/golden/ap_remote_pos_seq.delta.gz), every timed "
+                      "loc->pos answer == the oracle's (tests/golden/ap_remote_seq_pos.delta.gz), and they "
+                      "round-trip",
             "queries_vs_oracle_fixture": q_gold,
+            "loc_queries_vs_oracle_fixture": q_gold_loc,
             "queries_ok": q_ok,
             "world_size": dist.get_world_size() if dist is not None else 1,
             "per_rank_ops_s": [n_ops_doc * n * args.steps / t for t in per_rank],

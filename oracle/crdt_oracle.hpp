@@ -94,10 +94,26 @@ struct NodeBase {
   bool leaf;
   Internal* parent;  // nullptr = parent is the tree root
 };
+// L_UNBOUNDED: the "leaf = infinity" layout of SURVEY 8(c) (one leaf that never splits, so every
+// append / prepend of insert_internal applies), against which the release layout's results are
+// compared to detect where the leaf layout leaks into them (doc.rs:207, span.rs:61-64).
+constexpr u32 L_UNBOUNDED = 0x7FFFFFFFu;
 struct Leaf : NodeBase {
-  Span data[33];  // [0, cap) used; data[cap] stays default (guards data[num_entries] reads)
+  Span* data;     // [0, cap) used; data[cap] stays default (guards data[num_entries] reads)
   u32 n = 0;
-  Leaf() { leaf = true; parent = nullptr; }
+  Span inl[33];   // the release / debug layouts
+  std::vector<Span> big;  // the unbounded leaf (grows)
+  explicit Leaf(u32 cap) {
+    leaf = true;
+    parent = nullptr;
+    if (cap <= 32) data = inl;
+    else { big.resize(64); data = big.data(); }
+  }
+  void room(u32 need) {  // the unbounded leaf: storage for `need` entries + the default guard
+    if (big.empty() || need + 1 <= big.size()) return;
+    big.resize(2 * (size_t)(need + 1));
+    data = big.data();
+  }
 };
 struct Internal : NodeBase {
   u32 cnt[16];
@@ -126,10 +142,10 @@ struct Tree {
   bool track_index = true;
 
   Tree(u32 L_, u32 NC_) : L(L_), NC(NC_) {
-    leaves.emplace_back(new Leaf());
+    leaves.emplace_back(new Leaf(L));
     root = leaves.back().get();
   }
-  Leaf* new_leaf() { leaves.emplace_back(new Leaf()); return leaves.back().get(); }
+  Leaf* new_leaf() { leaves.emplace_back(new Leaf(L)); return leaves.back().get(); }
   Internal* new_internal() { internals.emplace_back(new Internal()); return internals.back().get(); }
 
   void notify(const Span& e, Leaf* leaf);
@@ -350,6 +366,7 @@ struct Tree {
         rem_moved = true;
       }
     } else {
+      node->room(filled + space);
       if (filled > c.idx) std::memmove(&node->data[c.idx + space], &node->data[c.idx], sizeof(Span) * (filled - c.idx));
       node->n += space;
     }

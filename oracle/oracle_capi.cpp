@@ -100,6 +100,8 @@ double now_s() {
 extern "C" {
 
 void* orc_doc_new(uint32_t leaf_cap, uint32_t node_cap, int track_index) {
+  // leaf_cap 0: the unbounded leaf (L_UNBOUNDED, crdt_oracle.hpp)
+  if (leaf_cap == 0) return new Doc(L_UNBOUNDED, 16, track_index != 0, false);
   if (leaf_cap < 4 || leaf_cap > 32 || node_cap < 8 || node_cap > 16) return nullptr;
   return new Doc(leaf_cap, node_cap, track_index != 0, track_index == 2);  // 2: the SplitList index
 }

@@ -1,7 +1,7 @@
 # Round 4 A/B on one box: (optionally) the GPU tests on the new library, then alternating clean
 # k_replay launches of the base and new libraries on 8,192 automerge-paper remote documents, and
 # (EXTRA=1) config 5 (1,024 docs), config 4 (16,384 docs) and kevin (one document + 64).
-# usage: TAG=v1 TESTS=1 EXTRA=0 bash scripts/gpu_r4_ab.sh
+# usage: TAG=v1 TESTS=1 EXTRA=0 [LIBS="a.so b.so"] bash scripts/gpu_r4_ab.sh
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -13,7 +13,9 @@ if [ "${TESTS:-1}" = 1 ]; then
   tail -1 gpurun_out/gpu_tests_$TAG.log
   [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/gpu_tests_$TAG.log | head -20; exit 1; }
 fi
-for L in $B/libcrdt_gpu_base.so $B/libcrdt_gpu.so $B/libcrdt_gpu_base.so $B/libcrdt_gpu.so; do
+LIBS=${LIBS:-"libcrdt_gpu_base.so libcrdt_gpu.so"}
+for L in $LIBS $LIBS; do
+  L=$B/$L
   echo -n "ap8192 $(basename $L) "
   CRDT_GPU_LIB=$L timeout -k 10 120 python scripts/prof_replay.py --docs 8192 --clean | tail -1 || exit 1
 done

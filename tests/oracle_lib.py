@@ -229,3 +229,31 @@ class DoubleDeletes:
         out = np.zeros((256, 3), np.uint32)
         n = self.L.orc_dd_get(self.h, _p(out), 256)
         return [tuple(int(x) for x in r) for r in out[:n]]
+
+
+# ---- layout sensitivity (the oracle at leaf 32 and leaf infinity, Q2 counted)
+LEAF_UNBOUNDED = 0  # OracleDoc(LEAF_UNBOUNDED): one leaf that never splits (crdt_oracle.hpp L_UNBOUNDED)
+
+
+def layout_items(ex: dict):
+    """Item-level state of an exported document, in document order: (order, origin_left,
+    origin_right, deleted) per item.  A run's first item carries the run's origin_left, the others
+    their predecessor (span.rs:23-28 origin_left_at_offset)."""
+    raw = ex["raw"].astype(np.int64)
+    ln = np.abs(raw[:, 3].astype(np.int32)).astype(np.int64)
+    ent = np.repeat(np.arange(raw.shape[0]), ln)
+    off = np.arange(int(ln.sum())) - np.repeat(np.cumsum(ln) - ln, ln)
+    order = raw[ent, 0] + off
+    ol = np.where(off == 0, raw[ent, 1], order - 1)
+    return order, ol, raw[ent, 2], raw[ent, 3].astype(np.int32) < 0
+
+
+def compare_layouts(a: dict, b: dict) -> dict:
+    """Two exports of one history at different leaf layouts: same_order = the same items in the
+    same document order with the same deleted flags; ol_diff / orr_diff = items whose stored
+    origin differs (YjsSpan::prepend keeps the entry's origin_left, span.rs:61-64)."""
+    oa, la, ra, da = layout_items(a)
+    ob, lb, rb, db = layout_items(b)
+    if oa.shape != ob.shape or not (np.array_equal(oa, ob) and np.array_equal(da, db)):
+        return {"same_order": False}
+    return {"same_order": True, "ol_diff": int((la != lb).sum()), "orr_diff": int((ra != rb).sum())}

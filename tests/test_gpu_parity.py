@@ -92,6 +92,27 @@ def test_trace_remote_exact(name):
         assert_same(e.export(d), o.export())
     assert (e.digests() == np.uint64(o.digest())).all()
     check_queries(e, 1, o)
+    check_query_fixtures(e, 0, name)
+
+
+def check_query_fixtures(e, doc, name):
+    """The engine's pos -> loc and loc -> pos answers against the committed fixtures
+    (tests/golden/make_queries.py; the oracle's answers, pinned in tests/test_oracle.py)."""
+    from bench import golden_pos_seq, golden_seq_pos
+    if name == "automerge-paper":
+        gseq = golden_pos_seq(name)
+        ga, gs = e.pos_to_loc(np.full(gseq.shape, doc, np.uint32), np.arange(gseq.shape[0], dtype=np.uint32))
+        assert (ga == 0).all() and np.array_equal(gs, gseq)
+        gp, gd = golden_seq_pos(name)
+        seq = np.arange(gp.shape[0], dtype=np.uint32)
+        p, d = e.loc_to_pos(np.full(seq.shape, doc, np.uint32), np.zeros(seq.shape, np.uint16), seq)
+        assert np.array_equal(d, gd) and np.array_equal(p[d != 2], gp[d != 2])
+        return
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"queries_{name}.npz"))
+    a, s = e.pos_to_loc(np.full(z["pos"].shape, doc, np.uint32), z["pos"])
+    assert np.array_equal(a, z["pos_agent"]) and np.array_equal(s, z["pos_seq"])
+    p, d = e.loc_to_pos(np.full(z["loc_seq"].shape, doc, np.uint32), z["loc_agent"], z["loc_seq"])
+    assert np.array_equal(d, z["loc_deleted"]) and np.array_equal(p[d != 2], z["loc_pos"][d != 2])
 
 
 @pytest.mark.parametrize("name", ["sveltecomponent", "rustcode", "automerge-paper"])

@@ -310,3 +310,31 @@ def test_query_fixture_matches_oracle():
     assert gseq is not None and gseq.shape[0] == len(o)
     a, s = o.pos_to_loc(np.arange(len(o), dtype=np.uint32))
     assert (a == 0).all() and np.array_equal(s, gseq)
+
+
+def test_loc_query_fixtures_match_oracle():
+    # tests/golden/ap_remote_seq_pos.delta.gz (bench.py checks every timed loc -> pos answer against
+    # it): the oracle's (agent 0, seq) -> (pos, deleted) (Cursor::count_pos, cursor.rs:147-190) for
+    # every seq of automerge-paper's remote replay; queries_{rustcode,sveltecomponent}.npz: sampled
+    # pos -> loc and loc -> pos answers of those traces' remote replays
+    import sys
+    sys.path.insert(0, os.path.dirname(HERE))
+    from bench import golden_seq_pos
+    o = OracleDoc(32, 16)
+    assert o.apply_remote_wire(load_remote_wire("automerge-paper")) == 0
+    gp, gd = golden_seq_pos("automerge-paper")
+    n = o.sizes()["next_order"]
+    assert gp.shape[0] == n
+    p, d = o.loc_to_pos(np.zeros(n, np.uint16), np.arange(n, dtype=np.uint32))
+    assert np.array_equal(d, gd) and np.array_equal(p[d != 2], gp[d != 2])
+    # every visible seq maps to its position and back (pos -> loc fixture)
+    a, s = o.pos_to_loc(np.arange(len(o), dtype=np.uint32))
+    assert np.array_equal(gp[s], np.arange(len(o))) and (gd[s] == 0).all()
+    for tr in ("rustcode", "sveltecomponent"):
+        z = np.load(os.path.join(HERE, "golden", f"queries_{tr}.npz"))
+        o = OracleDoc(32, 16)
+        assert o.apply_remote_wire(load_remote_wire(tr)) == 0
+        a, s = o.pos_to_loc(z["pos"])
+        assert np.array_equal(a, z["pos_agent"]) and np.array_equal(s, z["pos_seq"])
+        p, d = o.loc_to_pos(z["loc_agent"], z["loc_seq"])
+        assert np.array_equal(d, z["loc_deleted"]) and np.array_equal(p, z["loc_pos"])
