@@ -592,6 +592,7 @@ def main():
             "queries_ok": q_ok,
             "world_size": dist.get_world_size() if dist is not None else 1,
             "per_rank_ops_s": [n_ops_doc * n * args.steps / t for t in per_rank],
+            "build_id": crdt_amd.build_id(),
             "stage_s": stage_s,
             "stage_intern": "host" if args.host_intern else "device (k_intern)",
             "materialize": mat,

@@ -221,6 +221,10 @@ enum { CRDT_QUERY_LDS = 0, CRDT_QUERY_PER_THREAD = 1, CRDT_QUERY_MERGE = 2 };
 int crdt_set_query_kernel(crdt_engine* e, int mode);
 // Device bytes the engine holds (per-document pools, staged records, content, text).
 uint64_t crdt_mem_bytes(const crdt_engine* e);
+// Device bytes the engines of this process hold through their own allocations now, and the most
+// they held at once since the last reset (a relayout -- growth, crdt_fit -- moves the pools one
+// at a time: its peak is the old pools + the largest new one).  Diagnostic; never fails.
+int crdt_device_bytes(uint64_t* current, uint64_t* peak, int reset_peak);
 // Config 1's per-op check: after txn t (of every listed document), ask pos_to_loc(probes[t].pos)
 // and loc_to_pos(probes[t].agent, probes[t].seq) on the state reached so far (the README's two
 // mappings, cursor.rs:147-190 count_pos; answers as crdt_pos_to_loc / crdt_loc_to_pos).
@@ -238,6 +242,9 @@ int crdt_last_timings(crdt_engine* e, double* replay_ms, double* publish_ms);
 void* crdt_stream(crdt_engine* e);
 /* Text of the last HIP error seen by this thread (empty if none). */
 const char* crdt_last_error(void);
+/* The source hash this library was built from (crdt_amd.build(): sha256 over the sources and the
+ * build line, also stored beside the library), so a run can prove which sources it executed. */
+const char* crdt_build_id(void);
 
 #ifdef __cplusplus
 }

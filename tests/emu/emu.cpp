@@ -1,7 +1,9 @@
 // TEST INFRASTRUCTURE: runs replay_core.h on the CPU (WaveCPU backend) for single documents,
 // using the same host planning code as the engine, and exports the resulting state in the
 // oracle's export format so tests can diff the GPU algorithm against the oracle without a GPU.
+#define CRDT_EMU_CHECKS 1  // replay preconditions checked (crdt_types.h CRDT_EXPECT)
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>

@@ -115,6 +115,7 @@ struct WaveCPU {
   u32 cget_order(u32 i) const { return c[i & 63].order; }
   i32 cget_len(u32 i) const { return c[i & 63].len; }
   void cset(u32 i, const Span& s) { c[i & 63] = s; }
+  void cset_len(u32 i, i32 len) { c[i & 63].len = len; }
   template <class F> void cset_lanes(u32 a, u32 b, F f) { for (u32 l = a; l < b && l < 64; l++) c[l] = f(l); }
   u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
   void rank_load(const AgentRec*, u32) const {}

@@ -211,3 +211,54 @@ def test_fit_then_replay():
     o2 = OracleDoc()
     o2.apply_trace(o2.agent("jeremy"), t.counts, t.patches)
     assert int(e.digests()[1]) == o2.digest()
+
+
+def test_relayout_peak_memory():
+    # layout() moves the pools one at a time (k_relayout_pool: allocate the new pool, move every
+    # document's part, free the old one), so a growth relayout peaks at the old pools + the
+    # largest new one -- below 1.3x the grown footprint -- and crdt_fit at the old pools + the
+    # largest fitted one (both sets at once before)
+    from crdt_amd.traces import load_trace
+    t = load_trace("automerge-paper")
+    n = 64
+    e = crdt_amd.Engine(n, 32)
+    ag = int(e.agent_intern(list(range(n)), ["jeremy"] * n)[0])
+    half = t.counts.shape[0] // 2
+    ph = int(t.counts[:half].sum())
+    assert (e.apply_trace(list(range(n)), ag, t.counts[:half], t.patches[:ph]) == 0).all()
+    crdt_amd.Engine.device_bytes(reset_peak=True)
+    assert (e.apply_trace(list(range(n)), ag, t.counts[half:], t.patches[ph:]) == 0).all()
+    grown, peak = crdt_amd.Engine.device_bytes()
+    print(f"growth: footprint {grown / 1e6:.1f} MB, peak {peak / 1e6:.1f} MB ({peak / grown:.3f}x)")
+    assert peak <= 1.3 * grown
+    o = OracleDoc()
+    o.apply_trace(o.agent("jeremy"), t.counts, t.patches)
+    assert (e.digests() == np.uint64(o.digest())).all()
+    crdt_amd.Engine.device_bytes(reset_peak=True)
+    e.fit()
+    fitted, peak2 = crdt_amd.Engine.device_bytes()
+    print(f"fit: footprint {grown / 1e6:.1f} -> {fitted / 1e6:.1f} MB, peak {peak2 / 1e6:.1f} MB ({peak2 / grown:.3f}x)")
+    assert fitted <= grown and peak2 <= 1.5 * grown
+    e.reset_async()
+    e.run_async()
+    e.sync()
+    assert (e.status() == 0).all() and (e.digests() == np.uint64(o.digest())).all()
+
+
+def test_rejected_stage_leaves_agent_ids_unchanged():
+    # a stage call that names a document twice is CRDT_E_ARG before any interning: the agent ids a
+    # later valid call assigns follow the reference's get_or_create order (doc.rs:66-80) as if the
+    # rejected call had not happened
+    from crdt_amd.traces import load_remote_wire
+    w = load_remote_wire("sveltecomponent")
+    w2 = concurrent_wire(5, n_agents=4, rounds=3, ops_per_round=3)[0]
+    e = crdt_amd.Engine(2, 32)
+    with pytest.raises(crdt_amd.CrdtError):
+        e.apply_remote_wire([1, 1], [w2, w])
+    with pytest.raises(crdt_amd.CrdtError):
+        e.stage_random([0, 0], "zz", 10, 1)
+    assert e.apply_remote_wire([1], [w2])[0] == 0
+    o = OracleDoc()
+    assert o.apply_remote_wire(w2) == 0
+    assert_same(e.export(1), o.export())
+    assert int(e.digests()[1]) == o.digest()

@@ -33,16 +33,7 @@ class CrdtError(RuntimeError):
     pass
 
 
-def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defines: Sequence[str] = ()) -> str:
-    """Compile libcrdt_gpu.so for gfx950 with hipcc (in-tree).  `defines` only for diagnostic
-    builds written to another `out` (e.g. CRDT_PROF)."""
-    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [
-        os.path.join(INCLUDE, h) for h in ("crdt_gpu.h", "crdt_trace.h")]
-    if not force and os.path.exists(out):
-        lt = os.path.getmtime(out)
-        if all(os.path.getmtime(s) <= lt for s in srcs):
-            return out
-    os.makedirs(os.path.dirname(out), exist_ok=True)
+def _build_cmd(out: str, defines: Sequence[str]) -> list:
     # Codegen options for the replay's wave-uniform control flow (measured on k_replay, 8,192 AP
     # documents, scripts/gpu_ab.sh):
     #  -phi-elim-split-all-critical-edges: the fast paths have many early exits into one shared
@@ -50,17 +41,57 @@ def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defin
     #   are placed before every conditional branch and run whether it is taken or not (118 -> 110 ms);
     #  -structurizecfg-skip-uniform-regions: uniform branches stay plain s_cbranch_scc jumps instead
     #   of being structurized into exec-mask flow blocks with 64-bit boolean phis (109 -> 99 ms).
-    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-fno-strict-aliasing", "-mllvm", "-phi-elim-split-all-critical-edges=1",
-           "-mllvm", "-structurizecfg-skip-uniform-regions=1", "-I" + INCLUDE, "-I" + CSRC, "-o", out + ".tmp"] + ["-D" + d for d in defines] + [
-           os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "trace_ingest.cpp"), "-lz"]
+    return ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+            "-fno-strict-aliasing", "-mllvm", "-phi-elim-split-all-critical-edges=1",
+            "-mllvm", "-structurizecfg-skip-uniform-regions=1", "-I" + INCLUDE, "-I" + CSRC, "-o", out + ".tmp"] + [
+            "-D" + d for d in defines] + [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "trace_ingest.cpp"), "-lz"]
+
+
+def source_hash(defines: Sequence[str] = ()) -> str:
+    """sha256 (16 hex digits) over every source the library is built from (csrc/*, the public
+    headers) and the build line: what build() keys a rebuild on, embedded in the library
+    (crdt_build_id) and printed by __graft_entry__.smoke()."""
+    import hashlib
+    h = hashlib.sha256()
+    srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)) + [os.path.join(INCLUDE, x) for x in ("crdt_gpu.h", "crdt_trace.h")]
+    for p in srcs:
+        h.update(os.path.relpath(p, REPO).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(" ".join(_build_cmd("OUT", defines)[1:]).replace(REPO, "").encode())
+    return h.hexdigest()[:16]
+
+
+def build(force: bool = False, verbose: bool = False, out: str = LIB_PATH, defines: Sequence[str] = ()) -> str:
+    """Compile libcrdt_gpu.so for gfx950 with hipcc (in-tree).  The rebuild is keyed on
+    source_hash() (sources + build line), stored beside the library (`out` + ".srchash") and
+    embedded in it (crdt_build_id), not on file times.  `defines` only for diagnostic builds
+    written to another `out` (e.g. CRDT_PROF)."""
+    hsh = source_hash(defines)
+    stamp = out + ".srchash"
+    if not force and os.path.exists(out) and os.path.exists(stamp):
+        with open(stamp) as f:
+            if f.read().strip() == hsh:
+                return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = _build_cmd(out, list(defines) + [f'CRDT_SRC_HASH="{hsh}"'])
     r = subprocess.run(cmd, capture_output=not verbose, text=True)
     if r.returncode != 0:
         raise CrdtError("hipcc failed:\n" + (r.stderr or "")[-4000:])
     if not defines:  # (diagnostic builds, e.g. CRDT_PROF, may spill: they are never the product)
         check_codegen(out + ".tmp")
     os.replace(out + ".tmp", out)
+    with open(stamp, "w") as f:
+        f.write(hsh + "\n")
     return out
+
+
+def build_id(path: str = None) -> str:
+    """crdt_build_id() of the library `path` (default: the one lib() loads)."""
+    L = lib() if path is None else C.CDLL(path)
+    L.crdt_build_id.restype = C.c_char_p
+    return L.crdt_build_id().decode()
 
 
 # The replay's speed rests on its register budget: 8 waves per SIMD need <= 64 VGPRs (the 512-
@@ -168,6 +199,8 @@ def lib():
     L.crdt_apply_local_probed.argtypes = [vp, u64, P(u32), P(u64), vp, vp, vp, vp, P(i32)]
     L.crdt_mem_bytes.argtypes = [vp]
     L.crdt_mem_bytes.restype = u64
+    if hasattr(L, "crdt_device_bytes"):  # (older libraries, for A/B runs, lack it)
+        L.crdt_device_bytes.argtypes = [P(u64), P(u64), C.c_int]
     L.crdt_reset_async.argtypes = [vp]
     L.crdt_run.argtypes = [vp, P(i32)]
     L.crdt_run_async.argtypes = [vp]
@@ -210,9 +243,9 @@ EXPORTED_SYMBOLS = [
     "crdt_stage_remote_replicated", "crdt_reset_async", "crdt_run", "crdt_run_async", "crdt_publish_async",
     "crdt_sync", "crdt_pos_to_loc", "crdt_loc_to_pos", "crdt_pos_to_loc_dev_async", "crdt_loc_to_pos_dev_async",
     "crdt_doc_len", "crdt_doc_status", "crdt_digest", "crdt_export_sizes", "crdt_export", "crdt_last_timings",
-    "crdt_stream", "crdt_last_error", "crdt_stage_random", "crdt_debug_state",
+    "crdt_stream", "crdt_last_error", "crdt_build_id", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
-    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams", "crdt_set_device_intern", "crdt_set_query_kernel",
+    "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams", "crdt_set_device_intern", "crdt_set_query_kernel", "crdt_device_bytes",
     # include/crdt_trace.h (host-only trace ingestion)
     "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
@@ -406,6 +439,13 @@ class Engine:
     def mem_bytes(self) -> int:
         """device bytes held by the per-document pools + staged records"""
         return int(self.L.crdt_mem_bytes(self.h))
+
+    @staticmethod
+    def device_bytes(reset_peak: bool = False):
+        """(current, peak) device bytes held by this process's engines (crdt_device_bytes)"""
+        cur, peak = C.c_uint64(), C.c_uint64()
+        lib().crdt_device_bytes(C.byref(cur), C.byref(peak), int(reset_peak))
+        return cur.value, peak.value
 
     def reset_async(self):
         _check(self.L.crdt_reset_async(self.h), "reset")

@@ -27,6 +27,13 @@ typedef int64_t i64;
 #ifndef CRDT_STAT
 #define CRDT_STAT(k, v) ((void)0)
 #endif
+// Preconditions the replay relies on without testing them, checked by the CPU emulation (tests/emu
+// defines CRDT_EMU_CHECKS: the emulator parity tests abort on a violation); nothing on the GPU.
+#ifdef CRDT_EMU_CHECKS
+#define CRDT_EXPECT(c) do { if (!(c)) { fprintf(stderr, "replay precondition failed: %s (%s:%d)\n", #c, __FILE__, __LINE__); abort(); } } while (0)
+#else
+#define CRDT_EXPECT(c) ((void)0)
+#endif
 
 constexpr u32 ROOT_ORDER = 0xFFFFFFFFu;   // list/mod.rs:30
 constexpr u32 ROOT_AGENT = 0xFFFFu;       // "ROOT" -> AgentId::MAX (doc.rs:68)
@@ -41,7 +48,9 @@ constexpr u32 GROUP = 64;                 // directory slots per block (one wave
 // CU's LDS, so a document can have up to ROOT_CAP_MAX blocks = at least 32*(ROOT_CAP_MAX-1)
 // leaves (every block but the first holds >= 32 slots) = 13.9M entries at the release layout.
 constexpr u32 ROOT_CAP_MIN = 256;
-constexpr u32 ROOT_CAP_MAX = 13632;       // floor(163840 / 12 / 64) * 64 (two-level root's top entries)
+// (the two-level root's top entries: 12 B each + two words + the agent ranks within 160 KiB,
+// floor((163840 - 8 - 4 * RANK_LDS) / 12 / 64) * 64; static_assert below)
+constexpr u32 ROOT_CAP_MAX = 13568;
 // The flat LDS root also keeps a block -> group map (4 B per group: 16 B per group in all), so its
 // largest class is floor((163840 - 4 * RANK_LDS) / 16 / 64) * 64 groups; documents past it use
 // the two-level root.
@@ -50,6 +59,7 @@ constexpr u32 ROOT_CAP_LDS = 10176;
 // RANK_LDS agents sit in LDS next to the root while a wave replays (integrate's scan reads one per
 // scanned entry); documents with more read them from HBM.
 constexpr u32 RANK_LDS = 64;
+static_assert(12u * ROOT_CAP_MAX + 8u + 4u * RANK_LDS <= 163840u, "two-level root: one wave's LDS (engine.hip launch_shape) fits 160 KiB");
 // Past it the root has two levels (wave_gpu.h HR): LDS top entries of rows that hold 32..64 groups
 // each in HBM, up to ROOT_CAP_MAX - 64 top entries (LDS: 12 B each + two words) -- over 434k
 // groups, 13.9M leaves, 445M entries at the release layout.

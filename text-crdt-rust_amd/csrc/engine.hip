@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -30,15 +31,32 @@ thread_local std::string g_last_error;
     }                                                                                   \
   } while (0)
 
+// Device allocations of the engines of this process, with their current and peak total (the
+// relayout's peak footprint: crdt_device_bytes).
+std::mutex g_mem_mu;
+std::unordered_map<void*, u64> g_mem_size;
+u64 g_mem_cur = 0, g_mem_peak = 0;
 template <class T>
 hipError_t dalloc(T*& p, u64 n) {
   p = nullptr;
   if (n == 0) n = 1;
-  return hipMalloc((void**)&p, sizeof(T) * n);
+  hipError_t e = hipMalloc((void**)&p, sizeof(T) * n);
+  if (e == hipSuccess) {
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    g_mem_size[(void*)p] = sizeof(T) * n;
+    g_mem_cur += sizeof(T) * n;
+    g_mem_peak = std::max(g_mem_peak, g_mem_cur);
+  }
+  return e;
 }
 template <class T>
 void dfree(T*& p) {
-  if (p) (void)hipFree((void*)p);
+  if (p) {
+    (void)hipFree((void*)p);
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    auto it = g_mem_size.find((void*)p);
+    if (it != g_mem_size.end()) { g_mem_cur -= it->second; g_mem_size.erase(it); }
+  }
   p = nullptr;
 }
 
@@ -119,6 +137,29 @@ inline u32 hroot_top(u32 grp_cap) {  // LDS top entries per wave (a multiple of 
 }
 
 }  // namespace
+
+// Pools field `which` (kernels.h RL_*) := ptr; RL_ARUN also sets the agent table the move reads
+// the run bases from (src: the old table, dst: the new one).
+inline void set_pool_ptr(Pools& p, u32 which, void* ptr, AgentRec* agents) {
+  switch (which) {
+    case RL_LEAVES: p.leaves = (Span*)ptr; break;
+    case RL_SOL: p.slot_of_leaf = (u32*)ptr; break;
+    case RL_DIR_LEAF: p.dir_leaf = (u32*)ptr; break;
+    case RL_DIR_VIS: p.dir_vis = (u32*)ptr; break;
+    case RL_LEAF_OF: p.leaf_of = (u32*)ptr; break;
+    case RL_AGENT_OF: p.agent_of = (u16*)ptr; break;
+    case RL_CWO: p.cwo = (CwoRun*)ptr; break;
+    case RL_DELS: p.dels = (DelRun*)ptr; break;
+    case RL_DD: p.dd = (DDRun*)ptr; break;
+    case RL_DDB: p.ddb = (DDBlk*)ptr; break;
+    case RL_TXNS: p.txns = (TxnRec*)ptr; break;
+    case RL_PARENTS: p.parents = (u32*)ptr; break;
+    case RL_FRONTIER: p.frontier = (u32*)ptr; break;
+    case RL_GROUPS: p.groups = (GroupRec*)ptr; break;
+    case RL_ARUN: p.arun = (ARun*)ptr; p.agents = agents; break;
+    default: break;
+  }
+}
 
 struct crdt_engine {
   u32 L = 32;
@@ -288,7 +329,7 @@ struct crdt_engine {
   }
 
   // Assign per-document bases from docs[].caps into a fresh PoolSet; if `move`, relocate the
-  // existing state into it (k_relayout), else just install it.
+  // existing state into it (k_relayout_pool, one pool at a time), else just install it.
   int layout(bool move) {
     int r = 0;
     g_force_hroot = getenv("CRDT_FORCE_HBM_ROOT") != nullptr && getenv("CRDT_FORCE_HBM_ROOT")[0] == '1';
@@ -341,24 +382,8 @@ struct crdt_engine {
       s.rec_n = seg_h[d].rec_n;
       nseg[d] = s;
     }
-    HIPCHK(dalloc(np.leaves, nl * L));
-    HIPCHK(dalloc(np.sol, 2 * nl));  // {directory slot, successor leaf} per leaf
-    HIPCHK(dalloc(np.dir_leaf, nb * GROUP));
-    HIPCHK(dalloc(np.dir_vis, nb * GROUP));
-    HIPCHK(dalloc(np.leaf_of, nm));
-    HIPCHK(dalloc(np.agent_of, any_agent_map ? nm : 1));
-    HIPCHK(dalloc(np.hrows, any_hroot ? nhr * HROOT_ROW : 1));
-    HIPCHK(dalloc(np.gsob, any_hroot ? nb : 1));
-    HIPCHK(dalloc(np.cwo, nc));
-    HIPCHK(dalloc(np.arun, na));
-    HIPCHK(dalloc(np.dels, ndl));
-    HIPCHK(dalloc(np.dd, ndd * DD_BLK));
-    HIPCHK(dalloc(np.ddb, ndd));
-    HIPCHK(dalloc(np.txns, nt));
-    HIPCHK(dalloc(np.parents, npar));
-    HIPCHK(dalloc(np.frontier, nfr));
-    HIPCHK(dalloc(np.groups, nb));
-    HIPCHK(dalloc(np.agents, nag));
+    // sizes of the new pools (element counts; 0 -> one element)
+    const u64 n_agent_of = any_agent_map ? nm : 1, n_hrows = any_hroot ? nhr * HROOT_ROW : 1, n_gsob = any_hroot ? nb : 1;
     np.bytes = nl * L * 16 + nl * 8 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) +
                (any_hroot ? nhr * HROOT_ROW * 4 + nb * 4 : 0) + nc * 16 + na * 16 + ndl * 12 +
                ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * (u64)sizeof(AgentRec) + nfr * 4 + nb * 16;
@@ -367,6 +392,7 @@ struct crdt_engine {
               (unsigned long long)nl, (unsigned long long)nb, (unsigned long long)nm, (unsigned long long)nc,
               (unsigned long long)na, (unsigned long long)ndl, (unsigned long long)ndd, (unsigned long long)nt,
               (unsigned long long)npar, (unsigned long long)nag, (unsigned long long)nfr, np.bytes / 1e6);
+    HIPCHK(dalloc(np.agents, nag));  // (the new agent table first: the run move reads its bases)
     if (!agent_tab.empty())
       HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(n_agents_d, n_agents.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
@@ -376,18 +402,55 @@ struct crdt_engine {
       HIPCHK(hipMemcpyAsync(old_segs, segs, n_docs * sizeof(DocSeg), hipMemcpyDeviceToDevice, stream));
     }
     HIPCHK(hipMemcpyAsync(segs, nseg.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
-    if (move) {
-      Pools src = pools_view(pools), dst = pools_view(np);
-      if (L == 32) hipLaunchKernelGGL(k_relayout<32>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs);
-      else hipLaunchKernelGGL(k_relayout<4>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs);
+    // Pool by pool: allocate the new one, move every document's part (k_relayout_pool), free the
+    // old one.  The peak is the old pools + the largest new pool (2x both sets before).
+    auto step = [&](auto& old_p, auto& new_p, u64 count, u32 which) -> int {
+      HIPCHK(dalloc(new_p, count));
+      if (move && which < RL_N) {
+        Pools src = pools_view(pools), dst = pools_view(pools);
+        set_pool_ptr(src, which, (void*)old_p, pools.agents);
+        set_pool_ptr(dst, which, (void*)new_p, np.agents);
+        if (L == 32) hipLaunchKernelGGL(k_relayout_pool<32>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs, which);
+        else hipLaunchKernelGGL(k_relayout_pool<4>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs, which);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(stream));
+      }
+      dfree(old_p);
+      old_p = new_p;
+      return 0;
+    };
+    r = 0;
+    if (!r) r = step(pools.leaves, np.leaves, nl * L, RL_LEAVES);
+    if (!r) r = step(pools.sol, np.sol, 2 * nl, RL_SOL);  // {directory slot, successor leaf} per leaf
+    if (!r) r = step(pools.dir_leaf, np.dir_leaf, nb * GROUP, RL_DIR_LEAF);
+    if (!r) r = step(pools.dir_vis, np.dir_vis, nb * GROUP, RL_DIR_VIS);
+    if (!r) r = step(pools.leaf_of, np.leaf_of, nm, RL_LEAF_OF);
+    if (!r) r = step(pools.agent_of, np.agent_of, n_agent_of, RL_AGENT_OF);
+    if (!r) r = step(pools.hrows, np.hrows, n_hrows, RL_N);  // (rebuilt from the groups at every launch)
+    if (!r) r = step(pools.gsob, np.gsob, n_gsob, RL_N);
+    if (!r) r = step(pools.cwo, np.cwo, nc, RL_CWO);
+    if (!r) r = step(pools.dels, np.dels, ndl, RL_DELS);
+    if (!r) r = step(pools.dd, np.dd, ndd * DD_BLK, RL_DD);
+    if (!r) r = step(pools.ddb, np.ddb, ndd, RL_DDB);
+    if (!r) r = step(pools.txns, np.txns, nt, RL_TXNS);
+    if (!r) r = step(pools.parents, np.parents, npar, RL_PARENTS);
+    if (!r) r = step(pools.frontier, np.frontier, nfr, RL_FRONTIER);
+    if (!r) r = step(pools.groups, np.groups, nb, RL_GROUPS);
+    if (!r) r = step(pools.arun, np.arun, na, RL_ARUN);
+    if (r) { dfree(old_segs); return r; }
+    if (move) {  // the agents' run counts and last-run copies into the new table
+      Pools src = pools_view(pools), dst = pools_view(pools);
+      dst.agents = np.agents;
+      if (L == 32) hipLaunchKernelGGL(k_relayout_pool<32>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs, (u32)RL_AGENTS);
+      else hipLaunchKernelGGL(k_relayout_pool<4>, dim3((u32)n_docs), dim3(256), 0, stream, src, dst, old_segs, n_agents_d, (u32)n_docs, (u32)RL_AGENTS);
       HIPCHK(hipGetLastError());
-      HIPCHK(hipStreamSynchronize(stream));
-      dfree(old_segs);
-    } else {
-      HIPCHK(hipStreamSynchronize(stream));
     }
-    pools.free_all();
-    pools = np;
+    HIPCHK(hipStreamSynchronize(stream));
+    dfree(old_segs);
+    dfree(pools.agents);
+    pools.agents = np.agents;
+    np.agents = nullptr;
+    pools.bytes = np.bytes;
     seg_h = nseg;
     r = plan_classes();
     if (r) return r;
@@ -1015,6 +1078,16 @@ struct crdt_engine {
 };
 
 static bool valid(const crdt_engine* e) { return e && e->n_docs > 0; }
+// The documents a stage call names: in range and none twice (checked before any interning, so a
+// rejected call leaves every agent table -- and so the agent ids of later calls -- unchanged)
+static bool ids_ok(const crdt_engine* e, uint64_t n, const uint32_t* docs) {
+  std::vector<char> seen(e->n_docs, 0);
+  for (uint64_t i = 0; i < n; i++) {
+    if (docs[i] >= e->n_docs || seen[docs[i]]) return false;
+    seen[docs[i]] = 1;
+  }
+  return true;
+}
 
 extern "C" {
 
@@ -1193,6 +1266,7 @@ static int stage_local_impl(crdt_engine* e, uint64_t n_docs, const uint32_t* doc
                             const crdt_local_txn* txns, const crdt_local_op* ops,
                             const crdt_probe* probes = nullptr, std::vector<std::vector<u32>>* probe_rec = nullptr) {
   if (!valid(e) || !docs || !txn_off || (!txns && txn_off[n_docs]) ) return CRDT_E_ARG;
+  if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   if (probe_rec) probe_rec->assign(n_docs, {});
   std::vector<u64> ids(n_docs);
   std::vector<std::vector<Rec>> streams(n_docs);
@@ -1249,6 +1323,7 @@ int crdt_stage_local_shared(crdt_engine* e, uint64_t n_docs, const uint32_t* doc
                             uint32_t n_streams, const uint64_t* stream_txn_off, const crdt_local_txn* txns,
                             const crdt_local_op* ops) {
   if (!valid(e) || !docs || !stream_of_doc || !stream_txn_off || !n_streams) return CRDT_E_ARG;
+  if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   std::vector<std::vector<Rec>> enc(n_streams);
   std::vector<StreamNeeds> snd(n_streams);
   u64 op = 0;
@@ -1273,6 +1348,7 @@ int crdt_stage_local_shared(crdt_engine* e, uint64_t n_docs, const uint32_t* doc
 int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint8_t* const* wire,
                            const uint64_t* wire_len) {
   if (!valid(e) || !docs || !wire || !wire_len) return CRDT_E_ARG;
+  if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   std::vector<u64> ids(n_docs);
   std::vector<std::vector<Rec>> streams(n_docs);
   std::vector<StreamNeeds> needs(n_docs);
@@ -1372,6 +1448,7 @@ int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t w
 int crdt_stage_random(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const char* agent, uint32_t n_ops,
                       uint64_t seed) {
   if (!valid(e) || !docs || !agent || n_ops == 0 || std::strcmp(agent, "ROOT") == 0) return CRDT_E_ARG;
+  if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   std::vector<u64> ids(n_docs);
   std::vector<std::vector<Rec>> streams(n_docs);
   std::vector<StreamNeeds> needs(n_docs);
@@ -1684,6 +1761,14 @@ int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23) {
   return 0;
 }
 
+int crdt_device_bytes(uint64_t* current, uint64_t* peak, int reset_peak) {
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  if (current) *current = g_mem_cur;
+  if (peak) *peak = g_mem_peak;
+  if (reset_peak) g_mem_peak = g_mem_cur;
+  return 0;
+}
+
 uint64_t crdt_mem_bytes(const crdt_engine* e) {
   if (!e) return 0;
   return e->pools.bytes + e->rec_cap * sizeof(Rec) + e->content_cap * 4 + e->text_cap * 4 + e->canon_alloc * 28 +
@@ -1747,6 +1832,11 @@ int crdt_last_materialize_ms(crdt_engine* e, double* ms) {
 }
 
 const char* crdt_last_error(void) { return g_last_error.c_str(); }
+
+#ifndef CRDT_SRC_HASH
+#define CRDT_SRC_HASH "unknown"
+#endif
+const char* crdt_build_id(void) { return CRDT_SRC_HASH; }
 
 }  // extern "C"
 

@@ -1,7 +1,7 @@
 // Device kernels of the engine.
 //   k_init      ListCRDT::new() per document (wave per document)
 //   k_replay    apply the staged record stream (wave per document, replay_core.h)
-//   k_relayout  move every document's state into re-sized pools (block per document)
+//   k_relayout_pool  move every document's part of one pool into its re-sized pool (block per document)
 //   k_publish   flat index build: canonical spans (can_append compaction of the leaf entries in
 //               document order), visible-prefix vpos, order->span scatter, digest
 //   k_pub_index the order->span index of k_publish's documents, built in LDS (block per document)
@@ -133,43 +133,60 @@ __device__ __forceinline__ void bcopy(T* dst, const T* src, u64 n) {
   for (u64 k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
 }
 
-// Move document state between pool sets (growth / re-staging).  src.st == dst.st.
+// Move one pool of document state into re-sized pools (growth / re-staging / fit; engine.hip layout: the pools move one at a time, each freed
+// before the next is allocated, so a relayout needs the old pools + the largest new one, not both
+// sets).  Block per document.  src / dst differ only in the pool being moved (and, for
+// RL_ARUN, in the agent tables: src.agents the old one, dst.agents the new one with its run
+// bases); RL_AGENTS moves the agents' run counts and last-run copies into the new table.
+enum : u32 { RL_LEAVES, RL_SOL, RL_DIR_LEAF, RL_DIR_VIS, RL_LEAF_OF, RL_AGENT_OF, RL_CWO, RL_DELS, RL_DD, RL_DDB,
+             RL_TXNS, RL_PARENTS, RL_FRONTIER, RL_GROUPS, RL_ARUN, RL_AGENTS, RL_N };
 template <int L>
-__global__ __launch_bounds__(256) void k_relayout(Pools src, Pools dst, const DocSeg* old_seg, const u32* new_n_agents, u32 n) {
+__global__ __launch_bounds__(256) void k_relayout_pool(Pools src, Pools dst, const DocSeg* old_seg, const u32* new_n_agents, u32 n,
+                                                       u32 which) {
   u32 d = blockIdx.x;
   if (d >= n) return;
   DocState s = dst.st[d];
   DocSeg o = old_seg[d];
   DocSeg w = dst.seg[d];
-  bcopy(dst.leaves + w.leaf_base * L, src.leaves + o.leaf_base * L, (u64)s.n_leaves * L);
-  bcopy(dst.slot_of_leaf + 2 * w.leaf_base, src.slot_of_leaf + 2 * o.leaf_base, 2ull * s.n_leaves);
-  bcopy(dst.dir_leaf + w.blk_base * GROUP, src.dir_leaf + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
-  bcopy(dst.dir_vis + w.blk_base * GROUP, src.dir_vis + o.blk_base * GROUP, (u64)s.n_blocks * GROUP);
-  if (w.flags & o.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);
-  if (w.flags & o.flags & DOC_TRACK_AGENT) bcopy(dst.agent_of + w.map_base, src.agent_of + o.map_base, s.next_order);
-  bcopy(dst.cwo + w.cwo_base, src.cwo + o.cwo_base, s.n_cwo);
-  bcopy(dst.dels + w.del_base, src.dels + o.del_base, s.n_del);
-  bcopy(dst.dd + w.dd_base * DD_BLK, src.dd + o.dd_base * DD_BLK, (u64)s.n_ddb * DD_BLK);
-  bcopy(dst.ddb + w.dd_base, src.ddb + o.dd_base, s.n_ddb);
-  bcopy(dst.txns + w.txn_base, src.txns + o.txn_base, s.n_txn);
-  bcopy(dst.parents + w.par_base, src.parents + o.par_base, s.n_par);
-  bcopy(dst.frontier + w.fr_base, src.frontier + o.fr_base, s.n_fr);
-  bcopy(dst.groups + w.grp_base, src.groups + o.grp_base, s.ng);
-  for (u32 a = 0; a < s.n_agents; a++) {
-    AgentRec ao = src.agents[o.agent_base + a];
-    AgentRec an = dst.agents[w.agent_base + a];
-    bcopy(dst.arun + w.arun_base + an.run_base, src.arun + o.arun_base + ao.run_base, ao.run_cnt);
-    __syncthreads();
-    if (threadIdx.x == 0) {  // (the run count and the copy of the last run move; base / cap are the new layout's)
-      AgentRec* q = dst.agents + w.agent_base + a;
-      q->run_cnt = ao.run_cnt;
-      q->tkey = ao.tkey;
-      q->torder = ao.torder;
-      q->tlen = ao.tlen;
-    }
+  switch (which) {
+    case RL_LEAVES: bcopy(dst.leaves + w.leaf_base * L, src.leaves + o.leaf_base * L, (u64)s.n_leaves * L); break;
+    case RL_SOL: bcopy(dst.slot_of_leaf + 2 * w.leaf_base, src.slot_of_leaf + 2 * o.leaf_base, 2ull * s.n_leaves); break;
+    case RL_DIR_LEAF: bcopy(dst.dir_leaf + w.blk_base * GROUP, src.dir_leaf + o.blk_base * GROUP, (u64)s.n_blocks * GROUP); break;
+    case RL_DIR_VIS: bcopy(dst.dir_vis + w.blk_base * GROUP, src.dir_vis + o.blk_base * GROUP, (u64)s.n_blocks * GROUP); break;
+    case RL_LEAF_OF:
+      if (w.flags & o.flags & DOC_TRACK_MAP) bcopy(dst.leaf_of + w.map_base, src.leaf_of + o.map_base, s.next_order);
+      break;
+    case RL_AGENT_OF:
+      if (w.flags & o.flags & DOC_TRACK_AGENT) bcopy(dst.agent_of + w.map_base, src.agent_of + o.map_base, s.next_order);
+      break;
+    case RL_CWO: bcopy(dst.cwo + w.cwo_base, src.cwo + o.cwo_base, s.n_cwo); break;
+    case RL_DELS: bcopy(dst.dels + w.del_base, src.dels + o.del_base, s.n_del); break;
+    case RL_DD: bcopy(dst.dd + w.dd_base * DD_BLK, src.dd + o.dd_base * DD_BLK, (u64)s.n_ddb * DD_BLK); break;
+    case RL_DDB: bcopy(dst.ddb + w.dd_base, src.ddb + o.dd_base, s.n_ddb); break;
+    case RL_TXNS: bcopy(dst.txns + w.txn_base, src.txns + o.txn_base, s.n_txn); break;
+    case RL_PARENTS: bcopy(dst.parents + w.par_base, src.parents + o.par_base, s.n_par); break;
+    case RL_FRONTIER: bcopy(dst.frontier + w.fr_base, src.frontier + o.fr_base, s.n_fr); break;
+    case RL_GROUPS: bcopy(dst.groups + w.grp_base, src.groups + o.grp_base, s.ng); break;
+    case RL_ARUN:
+      for (u32 a = 0; a < s.n_agents; a++) {
+        AgentRec ao = src.agents[o.agent_base + a];
+        AgentRec an = dst.agents[w.agent_base + a];
+        bcopy(dst.arun + w.arun_base + an.run_base, src.arun + o.arun_base + ao.run_base, ao.run_cnt);
+      }
+      break;
+    case RL_AGENTS:
+      for (u32 a = threadIdx.x; a < s.n_agents; a += blockDim.x) {
+        AgentRec ao = src.agents[o.agent_base + a];  // (run base / cap: the new layout's)
+        AgentRec* q = dst.agents + w.agent_base + a;
+        q->run_cnt = ao.run_cnt;
+        q->tkey = ao.tkey;
+        q->torder = ao.torder;
+        q->tlen = ao.tlen;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) dst.st[d].n_agents = new_n_agents[d];
+      break;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) dst.st[d].n_agents = new_n_agents[d];
 }
 
 // Order -> leaf map of documents that start keeping it (their first remote stream after local

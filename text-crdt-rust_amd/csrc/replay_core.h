@@ -1664,6 +1664,13 @@ struct Replayer {
       i32 el = w.cget_len(c.idx);
       if (el <= 0) break;
       if (c.off + l > (u32)el) break;
+      if (back & (el == 1)) {  // a one-item entry: mutate_entry deactivates it in place (mutations.rs:265-273)
+        w.cset_len(c.idx, -1);
+        p(C_NOW, g(C_NOW) - 1u);
+        p(C_DIRTY, 1u);
+        done++;
+        continue;
+      }
       CRDT_STAT(back ? 48 : 49, 1); CRDT_STAT(52, c.off == 0u);
 #ifdef CRDT_PROF_LOOP
       u64 q1 = w.clock();
@@ -1679,7 +1686,10 @@ struct Replayer {
       done++;
       if (done == k) break;
       u32 t2 = back ? t1 - done : t1 + done;
-      if (!find_order(t2, true, c)) break;
+      // (backspacing from inside an entry: the item before the deleted one ends the entry's first
+      // part, which stays at its index of the cached leaf -- no lookup)
+      if (back & (c.off != 0u)) c.off -= 1u;
+      else if (!find_order(t2, true, c)) break;
       el = w.cget_len(c.idx);
       if (el <= 0) break;
       if (c.off + l > (u32)el) break;
@@ -1851,6 +1861,7 @@ struct Replayer {
     u32 len = (u32)item.len;
     u32 has_rem = off < slen(e);
     u32 space = 1u + has_rem;  // (fits: the caller sent n + space > L to the split path)
+    CRDT_EXPECT(n + space <= (u32)L);
     if (g(K_MAP) - item.order < len) return 0;
     // entry writes straight to the cache (truncating e keeps its visible items in e + rem); the
     // visible count grows by exactly the item's len
@@ -2319,6 +2330,8 @@ struct Replayer {
 #else
           if (!fast_txn(pos, REC_LTXN, 1u, gh, go)) break;
 #endif
+          // (the loop skips fast_txn_ok: every fast commit keeps it true and keeps a cached leaf)
+          CRDT_EXPECT(g(F_FAST) == 1u && g(C_LEAF) != INVALID);
           done++;
         }
         p(S_GEN_DONE, done);

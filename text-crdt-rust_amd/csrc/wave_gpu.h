@@ -372,6 +372,7 @@ struct WaveGPU {
     er = wrlane(er, s.orr, i);
     en = (i32)wrlane((u32)en, (u32)s.len, i);
   }
+  __device__ __forceinline__ void cset_len(u32 i, i32 len) { en = (i32)wrlane((u32)en, (u32)len, i); }
   // entries [a, b) := f(lane), lane-parallel (f computes each lane's entry in VALU)
   template <class F> __device__ __forceinline__ void cset_lanes(u32 a, u32 b, F f) {
     u32 l = lane();
