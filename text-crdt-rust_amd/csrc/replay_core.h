@@ -427,6 +427,12 @@ struct Replayer {
     w.cset(idx, e);
     p(C_DIRTY, 1u);
   }
+  CRDT_HD u32 olc_stat(u32 order, const Cursor& left) {  // (statistics build only: 1 cached leaf, 2 left's leaf, 0 another, 3 ROOT)
+    if (order == ROOT_ORDER) return 3;
+    if (g(C_LEAF) != INVALID && w.cfind_order(g(C_N), order) >= 0) return 1;
+    u32 lf = w.ld(w.at(lof(), order));
+    return lf == left.leaf ? 2 : 0;
+  }
   CRDT_HD static u32 clen_i(i32 len) { return len > 0 ? (u32)len : 0u; }
   CRDT_HD static u32 slen_i(i32 len) { return (u32)(len < 0 ? -len : len); }
   CRDT_HD u32 cur_len() const { return g(S_LEN) + g(C_NOW) - g(C_VIS); }
@@ -589,7 +595,7 @@ struct Replayer {
     u32 rl = w.row_ld(dleaf(blk)), rv = w.row_ld(dvis(blk));
     u32 nl = g(S_N_LEAVES);
     p(S_N_LEAVES, nl + 1);
-    CRDT_STAT(0, 1); CRDT_STAT(1, g(C_N) - idx); CRDT_STAT(16 + idx, 1);
+    CRDT_STAT(0, 1); CRDT_STAT(1, g(C_N) - idx); CRDT_STAT(16 + (idx & 15u), 1);
     // the leaf list: nl goes right after the cached leaf
     u32 osucc = cached_succ_leaf();
     w.st(w.template at<2>(sol(), nl) + 1, osucc == INVALID ? END_LEAF : osucc);
@@ -1092,6 +1098,7 @@ struct Replayer {
   // inl: the txn's single op (and for a remote txn its single parent) are gop / gpar, not records
   // after the header (a compact record, or a generated op)
   CRDT_HD i32 apply_txn(const Rec& h, u32 pos, bool remote, u32 inl, const Rec& gop, const Rec& gpar) {
+    CRDT_STAT(47, 1);
 #ifdef CRDT_PROF
     u64 prof_t0 = w.clock();
 #endif
@@ -1227,6 +1234,7 @@ struct Replayer {
             if (g(K_AGMAP)) {
               u32 nn = g(C_N), last, last_scan;
               u32 na = g(S_N_AGENTS);
+              CRDT_STAT(45, 1); CRDT_STAT(46, nn - c.idx);
               u32 f = w.scan_batch(c.idx, nn, item.ol, item.orr, w.rank_of(agents(), na, agent), oag(), agents(), na,
                                    g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT), last, last_scan);
               if (last != INVALID) {
@@ -1247,6 +1255,7 @@ struct Replayer {
           if (other_order == item.orr) break;
           Span oe = w.cget(c.idx);  // get_item ensured c.leaf
           Cursor olc;
+          CRDT_STAT(40, 1); CRDT_STAT(41 + olc_stat(origin_left_at_offset(oe, c.off), left), 1);
           if (!cursor_after(origin_left_at_offset(oe, c.off), false, olc)) return ST_UNKNOWN_ID;
           int r = cmp(olc, left);
           if (r < 0) break;

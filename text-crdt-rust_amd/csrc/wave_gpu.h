@@ -490,19 +490,24 @@ struct WaveGPU {
   }
   __device__ __forceinline__ void cache_from_moved() { eo = mo; el = ml; er = mr; en = (i32)mn; }
   // lof[order + t] = v for every item of the entries in lanes [a, b): 64 items per step, each
-  // lane finding its entry by a 6-step search over the entries' length prefix
+  // lane finding its entry by a binary search over the entries' length prefix (entries sit in
+  // lanes < L: log2(L) steps, on bpermute byte addresses), then the item's order from one more
+  // bpermute of (entry order - entry start)
   __device__ __forceinline__ void fill_runs(u32* base, u32 a, u32 b, u32 v) const {
     u32 l = lane();
     u32 ln = l >= a && l < b ? (u32)(en < 0 ? -en : en) : 0u;
     u32 Pi = wave_incl_scan(ln);
     u32 T = rdlane(Pi, 63);
+    u32 vb = eo - (Pi - ln);  // item j (of all the entries' items) of this lane's entry: order vb + j
     for (u32 t = 0; t < T; t += 64) {
       u32 j = t + l;
-      u32 m = 0;
-      for (u32 step = (u32)L / 2u; step; step >>= 1)  // (entries sit in lanes < L: m < L)
-        if (shfl(Pi, m + step - 1u) <= j) m += step;
-      u32 pm = shfl(Pi, m), lm = shfl(ln, m), om = shfl(eo, m);
-      if (j < T) base[om + (j - (pm - lm))] = v;
+      u32 m4 = 0;  // 4 x the entry's lane (a bpermute byte address)
+      for (u32 step = (u32)L / 2u; step; step >>= 1) {
+        u32 x = (u32)__builtin_amdgcn_ds_bpermute((int)(m4 + 4u * (step - 1u)), (int)Pi);
+        m4 = x <= j ? m4 + 4u * step : m4;
+      }
+      u32 o = (u32)__builtin_amdgcn_ds_bpermute((int)m4, (int)vb) + j;
+      if (j < T) *(u32*)((char*)base + (u64)(o * 4u)) = v;
     }
   }
   __device__ __forceinline__ void cache_clear(u32 a, u32 b) {
