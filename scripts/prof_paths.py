@@ -17,6 +17,19 @@ local = mode == "local"
 e = crdt_amd.Engine(n, 32)
 if mode == "random":  # config 4: 20,000 generated ops per document (bench_config4.py's shape)
     e.stage_random(list(range(n)), "gen", 20000, 0xC0FFEE)
+elif mode == "kevin":  # benches/yjs.rs:51-62 shape: single-char prepends (200,000 per document)
+    k = 200_000
+    class T:
+        counts = np.ones(k, np.uint32)
+        patches = np.zeros((k, 3), np.uint32)
+    T.patches[:, 2] = 1
+    e.share_streams(True)
+    ag = e.agent_intern(list(range(n)), ["seph"] * n)
+    e.stage_local_shared(list(range(n)), [0] * n, int(ag[0]), [T])
+elif mode == "config5":  # one seeded concurrent history (SURVEY 8(d) shape) on every document
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fuzz_gen import config5_wire
+    e.stage_remote_replicated(config5_wire(7, base_len=1 << 20, n_agents=16, rounds=64, ops=64), 0xFFFFFFFF, [""] * n)
 elif local:
     t = load_trace("automerge-paper")
     ag = e.agent_intern(list(range(n)), ["jeremy"] * n)
@@ -43,6 +56,12 @@ for i, k in enumerate(names):
 s = np.array([e.debug_state(d) for d in range(3, n, 4 * max(1, n // 256))]).astype(np.float64)[:, P0:P0 + 4].mean(axis=0)
 if mode == "random":
     print(f"  generated-op cycles by part: draw + op {s[0]:.4g}, fast path without cursor {s[1]:.4g}, cursor in leaf {s[2]:.4g}, leaf switch (commit + descent + load) {s[3]:.4g}")
+elif os.environ.get("PROF_TXN2"):  # a -DCRDT_PROF_TXN2 build: apply_txn's bookkeeping by part
+    print(f"  apply_txn cycles by part: prologue (author switch, fits, assign_order_to_client) {s[0]:.4g}, ops {s[1]:.4g}, "
+          f"parents {s[2]:.4g}, insert_txn (frontier, shadow, txns) {s[3]:.4g}")
+elif os.environ.get("PROF_TXN"):  # a -DCRDT_PROF_TXN build: apply_txn's cycles by part
+    print(f"  apply_txn cycles by part: txn bookkeeping (fits, orders, parents, insert_txn) {s[0]:.4g}, integrate scan {s[1]:.4g}, "
+          f"deletes (incl. double deletes) {s[2]:.4g}, op fetch + origins + insert_internal {s[3]:.4g}")
 elif os.environ.get("PROF_LOOP"):  # a -DCRDT_PROF_LOOP build: detail of the leaf-split loop
     print(f"  leaf-split loop cycles by part: delete_general without split_at {s[0]:.4g}, split_at {s[1]:.4g}, "
           f"find_order + checks {s[2]:.4g}, delete_segment {s[3]:.4g}")

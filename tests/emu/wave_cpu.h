@@ -10,6 +10,12 @@
 
 #include "crdt_types.h"
 
+// (statistics build of the emulator: counts of context / cache-lane accesses, the GPU's
+// v_readlane / v_writelane traffic)
+#ifndef WCPU_COUNT
+#define WCPU_COUNT(kind, f) ((void)0)
+#endif
+
 namespace crdt {
 
 template <int L>
@@ -22,9 +28,9 @@ struct WaveCPU {
 
   // context registers (plain array: slot f)
   u32 x[192] = {};
-  u32 xg(u32 f) const { return x[f]; }
+  u32 xg(u32 f) const { WCPU_COUNT(0, f); return x[f]; }
   template <class T> static T* gptr(u64 v) { return (T*)v; }
-  void xs(u32 f, u32 v) { x[f] = v; }
+  void xs(u32 f, u32 v) { WCPU_COUNT(1, f); x[f] = v; }
   void x_pin() {}
   void bind_root(const Pools&, const DocSeg&) {}
   void x_load_state(const DocState* p, u32 base) { std::memcpy(x + base, p, sizeof(DocState)); }
@@ -111,17 +117,21 @@ struct WaveCPU {
     return n;
   }
   void cache_store(Span* p) const { for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
-  Span cget(u32 i) const { return c[i & 63]; }
-  u32 cget_order(u32 i) const { return c[i & 63].order; }
-  i32 cget_len(u32 i) const { return c[i & 63].len; }
-  void cset(u32 i, const Span& s) { c[i & 63] = s; }
+  Span cget(u32 i) const { WCPU_COUNT(2, 0); return c[i & 63]; }
+  u32 cget_order(u32 i) const { WCPU_COUNT(3, 0); return c[i & 63].order; }
+  i32 cget_len(u32 i) const { WCPU_COUNT(3, 1); return c[i & 63].len; }
+  void cset(u32 i, const Span& s) { WCPU_COUNT(4, 0); c[i & 63] = s; }
   void cset_len(u32 i, i32 len) { c[i & 63].len = len; }
   template <class F> void cset_lanes(u32 a, u32 b, F f) { for (u32 l = a; l < b && l < 64; l++) c[l] = f(l); }
   u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
   void rank_load(const AgentRec*, u32) const {}
   u32 rank_of(const AgentRec* agents, u32, u32 a) const { return agents[a].rank; }
-  u32 scan_batch(u32 a, u32 n, u32 X, u32 orr, u32 my_rank, const u16* oag, const AgentRec* agents, u32 n_agents, u32 tkey,
+  mutable const u16* oag = nullptr;  // (scan_gather's map, read by scan_batch)
+  u32 scan_gather(u32, u32, const u16* m) const { oag = m; return 0u; }
+  u32 rank_row(u32) const { return 0u; }
+  u32 scan_batch(u32, u32, u32 me, u32 a, u32 n, u32 X, u32 orr, const AgentRec* agents, u32 n_agents, u32 tkey,
                  u32 tlen, u32 tagent, u32& last, u32& last_scan) const {
+    u32 my_rank = agents[me].rank;
     auto agent_of = [&](u32 o) -> u32 { return o - tkey < tlen ? tagent : oag[o]; };
     u32 f = n;
     for (u32 j = a; j < n; j++) {
@@ -167,6 +177,9 @@ struct WaveCPU {
     }
   }
   void cache_from_moved() { for (u32 j = 0; j < 64; j++) c[j] = mv[j]; }
+  Span pfr[64];
+  void leaf_prefetch(const Span* p) { for (u32 j = 0; j < 64; j++) pfr[j] = j < (u32)L ? p[j] : Span{0, 0, 0, 0}; }
+  u32 cache_from_prefetch() { u32 n = 0; for (u32 j = 0; j < 64; j++) { c[j] = pfr[j]; n += c[j].len != 0; } return n; }
   void fill_runs(u32* base, u32 a, u32 b, u32 v) const {
     for (u32 i = a; i < b; i++) for (u32 t = 0; t < slen(c[i]); t++) base[c[i].order + t] = v;
   }

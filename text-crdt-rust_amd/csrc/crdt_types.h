@@ -48,18 +48,26 @@ constexpr u32 GROUP = 64;                 // directory slots per block (one wave
 // CU's LDS, so a document can have up to ROOT_CAP_MAX blocks = at least 32*(ROOT_CAP_MAX-1)
 // leaves (every block but the first holds >= 32 slots) = 13.9M entries at the release layout.
 constexpr u32 ROOT_CAP_MIN = 256;
-// (the two-level root's top entries: 12 B each + two words + the agent ranks within 160 KiB,
-// floor((163840 - 8 - 4 * RANK_LDS) / 12 / 64) * 64; static_assert below)
+// (the two-level root's top entries: 12 B each + two words + the agent ranks + the prefetch row
+// within 160 KiB, floor((163840 - 8 - 4 * RANK_LDS - 4 * PF_LDS) / 12 / 64) * 64; static_assert below)
 constexpr u32 ROOT_CAP_MAX = 13568;
 // The flat LDS root also keeps a block -> group map (4 B per group: 16 B per group in all), so its
-// largest class is floor((163840 - 4 * RANK_LDS) / 16 / 64) * 64 groups; documents past it use
+// largest class is floor((163840 - 4 * RANK_LDS - 4 * PF_LDS) / 16 / 64) * 64 groups; documents past it use
 // the two-level root.
 constexpr u32 ROOT_CAP_LDS = 10176;
 // Agent ranks (the integrate tie-break's name order, doc.rs:207) of documents with at most
 // RANK_LDS agents sit in LDS next to the root while a wave replays (integrate's scan reads one per
 // scanned entry); documents with more read them from HBM.
 constexpr u32 RANK_LDS = 64;
-static_assert(12u * ROOT_CAP_MAX + 8u + 4u * RANK_LDS <= 163840u, "two-level root: one wave's LDS (engine.hip launch_shape) fits 160 KiB");
+// A wave's LDS slice (kernels.h wave_with_root): a 512 B leaf row integrate's scan prefetches the
+// successor leaf into (LDS-DMA), the root (flat: blk / cnt / vis / block -> group map, 4 u32 per
+// group; two-level: 3 u32 per top entry + 2 words) and the agent ranks; 16 B aligned.
+constexpr u32 PF_LDS = 128;
+CRDT_HD constexpr u32 wave_lds_words(u32 rcap, bool hr) {
+  return (PF_LDS + (hr ? 3u * rcap + 2u : 4u * rcap) + RANK_LDS + 3u) & ~3u;
+}
+static_assert(4u * wave_lds_words(ROOT_CAP_MAX, true) <= 163840u, "two-level root: one wave's LDS fits 160 KiB");
+static_assert(4u * wave_lds_words(ROOT_CAP_LDS, false) <= 163840u, "flat root: one wave's LDS fits 160 KiB");
 // Past it the root has two levels (wave_gpu.h HR): LDS top entries of rows that hold 32..64 groups
 // each in HBM, up to ROOT_CAP_MAX - 64 top entries (LDS: 12 B each + two words) -- over 434k
 // groups, 13.9M leaves, 445M entries at the release layout.

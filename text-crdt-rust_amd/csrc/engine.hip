@@ -115,7 +115,7 @@ inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
 // rcap top entries of 12 B + two words per wave; both + RANK_LDS agent ranks)
 struct LaunchShape { u32 wpb, rcap; size_t lds; };
 inline LaunchShape launch_shape(u32 rcap, bool hr = false) {
-  u32 per_wave = (hr ? 12u * rcap + 8u : 16u * rcap) + 4u * RANK_LDS;  // (+ the agent ranks)
+  u32 per_wave = 4u * wave_lds_words(rcap, hr);  // (+ the agent ranks and the scan's prefetch row)
   u32 wpb = std::max<u32>(1u, std::min<u32>(WAVES_PER_BLOCK, 163840u / per_wave));
   return LaunchShape{wpb, rcap, (size_t)wpb * per_wave};
 }

@@ -49,9 +49,9 @@ __device__ __forceinline__ u32 span_of_order(const PubOut& O, const DocSeg& seg,
 
 #define WAVES_PER_BLOCK 4
 
-// Dynamic LDS of the wave-per-document kernels: each wave's directory root (flat: 4 x rcap u32;
-// two-level: 3 x rcap + 2) and the document's agent ranks (RANK_LDS u32; launch shape:
-// engine.hip launch_shape).
+// Dynamic LDS of the wave-per-document kernels: each wave's slice (crdt_types.h wave_lds_words):
+// the scan's prefetch row, the directory root (flat: 4 x rcap u32; two-level: 3 x rcap + 2) and
+// the document's agent ranks (RANK_LDS u32; launch shape: engine.hip launch_shape).
 extern __shared__ u32 s_dyn[];
 template <int L, bool HR = false>
 __device__ __forceinline__ WaveGPU<L, HR> wave_with_root(u32 rcap) {
@@ -60,7 +60,8 @@ __device__ __forceinline__ WaveGPU<L, HR> wave_with_root(u32 rcap) {
   // a generic pointer would make them flat ops, whose waits also drain every pending store
   w.rcap = rcap;
   u32 root = HR ? 3u * rcap + 2u : 4u * rcap;
-  w.rt = (typename WaveGPU<L, HR>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * (root + RANK_LDS));
+  w.pf = (typename WaveGPU<L, HR>::lds_u32*)(s_dyn + uni(threadIdx.x >> 6) * wave_lds_words(rcap, HR));
+  w.rt = w.pf + PF_LDS;
   w.rk = w.rt + root;
   return w;
 }

@@ -118,6 +118,9 @@ struct Replayer {
   u32 prof_gen = 0;  // generated ops (config 4): detail = gen / fast path / cursor / leaf switch
   u32 prof_cur = 0, prof_sw = 0;  // cycles in cursor_at_content_pos and in its leaf switches
   u32 prof_split = 0;  // cycles in split_at (-DCRDT_PROF_LOOP: detail of fast_deletes' leaf-split loop)
+  // -DCRDT_PROF_TXN: apply_txn's cycles by part (txn bookkeeping / integrate's scan / deletes /
+  // op fetch + origins + insert_internal), added to the DocState counters of d % 4 == 3 documents
+  u32 pt_scan = 0, pt_del = 0, pt_ins = 0;
 #endif
 
   // ------------------------------------------------------------------ context access
@@ -338,7 +341,15 @@ struct Replayer {
     slot_of(leaf, blk, i);
     return (w.root_find_blk(g(S_NG), blk) << 6) | i;
   }
-  CRDT_HD u32 leaf_at_start() const { return w.ld(dleaf(w.root_blk(0))); }
+  // The first leaf of the document is always leaf 0: init_empty creates it in slot 0 of block 0,
+  // and leaves are only ever linked in after an existing one (split_at; blk_split moves the upper
+  // half of a block to a block after it), never before it or removed -- as the reference's
+  // leftmost leaf stays leftmost (root.rs:133-150).  (No directory lookup: an LDS read and a
+  // dependent load per insert at position 0 before.)
+  CRDT_HD u32 leaf_at_start() const {
+    CRDT_EXPECT(w.ld(dleaf(w.root_blk(0))) == 0u);
+    return 0u;
+  }
   CRDT_HD u32 leaf_at_end() const {
     u32 gg = g(S_NG) - 1;
     return w.ld(dleaf(w.root_blk(gg)) + w.root_cnt(gg) - 1);
@@ -420,6 +431,31 @@ struct Replayer {
     u32 slot, succ;
     w.ld_raw2(w.template at<2>(sol(), leaf), slot, succ);  // (one 8-byte load)
     load_cache(leaf, slot, succ);
+  }
+  // The successor of the cached leaf requested ahead: its entries (W::leaf_prefetch, into LDS) and
+  // its slot entry {slot, successor}, in flight while the cached leaf is scanned; INVALID: none.
+  CRDT_HD u32 prefetch_succ(u32& slot, u32& succ) {
+    u32 nl = cached_succ_leaf();
+    if (nl == INVALID) return INVALID;
+    w.leaf_prefetch(leafp(nl));
+    w.ld_raw2(w.template at<2>(sol(), nl), slot, succ);
+    return nl;
+  }
+  // ... made the cached leaf (load_cache with the entries already in registers)
+  CRDT_HD void switch_to_prefetched(u32 leaf, u32 slot, u32 succ) {
+    commit();
+    p(C_N, w.cache_from_prefetch());
+    u32 sl = w.uni_(slot);
+    p(C_LEAF, leaf);
+    p(C_BLK, sl >> 6);
+    p(C_I, sl & 63u);
+    p(C_DIRTY, 0);
+    u32 v = w.cache_vis_from(0u);
+    p(C_NOW, v);
+    p(C_VIS, v);
+    p(C_VSTART, VS_BAD);
+    p(C_SUCC, w.uni_(succ));
+    p(C_SUCC_ORD, INVALID);
   }
   // set entry idx of the cached leaf (tracks the cached visible count exactly)
   CRDT_HD void set(u32 idx, const Span& e) {
@@ -1130,6 +1166,9 @@ struct Replayer {
     u32 next = first;
     assign_order_to_client(agent, seq, first, txn_len);
     p(S_NEXT_ORDER, first + txn_len);
+#ifdef CRDT_PROF_TXN2
+    u64 prof_ta = w.clock();
+#endif
 
     u32 k = 0;
     u32 mode = M_FETCH;
@@ -1214,6 +1253,10 @@ struct Replayer {
       Span a0{0, 0, 0, 0}, a1{0, 0, 0, 0}, a2{0, 0, 0, 0};
       u32 n = 0;
       u32 home = INVALID;
+#ifdef CRDT_PROF_TXN
+      u64 pq0 = w.clock();
+      u32 pq_ins = mode == M_INS;
+#endif
       if (mode == M_INS) {
         // integrate (doc.rs:167-234): scan entries from the insertion point
         Cursor left = c, scan_start = c;
@@ -1235,15 +1278,22 @@ struct Replayer {
               u32 nn = g(C_N), last, last_scan;
               u32 na = g(S_N_AGENTS);
               CRDT_STAT(45, 1); CRDT_STAT(46, nn - c.idx);
-              u32 f = w.scan_batch(c.idx, nn, item.ol, item.orr, w.rank_of(agents(), na, agent), oag(), agents(), na,
+              // (the successor leaf is requested before this leaf is evaluated: a scan that runs
+              // through it finds it in LDS)
+              u32 ag = w.scan_gather(c.idx, nn, oag());
+              u32 rt = w.rank_row(na);
+              u32 pslot, psucc;
+              u32 pl = prefetch_succ(pslot, psucc);
+              u32 f = w.scan_batch(ag, rt, agent, c.idx, nn, item.ol, item.orr, agents(), na,
                                    g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT), last, last_scan);
               if (last != INVALID) {
                 scanning = last_scan != 0u;
                 if (last_scan) scan_start = Cursor{c.leaf, last, 0u};
               }
-              if (f >= nn) {  // no event in this leaf: on to the next one
-                c.idx = nn - 1u;
-                if (!next_entry(c)) return ST_NONTERMINATING;
+              if (f >= nn) {  // no event in this leaf: on to the next one (next_entry, cursor.rs:127-145)
+                if (pl == INVALID) return ST_NONTERMINATING;
+                switch_to_prefetched(pl, pslot, psucc);
+                c = Cursor{pl, 0u, 0u};
                 continue;
               }
               c.idx = f;
@@ -1321,9 +1371,20 @@ struct Replayer {
         if (remaining == 0) mode = (mode == M_LDEL && lins > 0) ? M_LINS : M_FETCH;
       }
       // ---------------------------------------------------------------- the one insert site
+#ifdef CRDT_PROF_TXN
+      u64 pq1 = w.clock();
+      if (pq_ins) pt_scan += (u32)(pq1 - pq0);
+      else pt_del += (u32)(pq1 - pq0);
+#endif
       if (!insert_items(a0, a1, a2, n, c, home)) return ST_INTERNAL;
+#ifdef CRDT_PROF_TXN
+      pt_ins += (u32)(w.clock() - pq1);
+#endif
     }
     if (!remote && next != first + txn_len) return ST_BAD_INPUT;
+#ifdef CRDT_PROF_TXN2
+    u64 prof_tb = w.clock();
+#endif
     u32 p0 = 0;
     if (remote) {
       u32* pp = par() + g(S_N_PAR);
@@ -1340,7 +1401,21 @@ struct Replayer {
 #ifdef CRDT_PROF
     u64 prof_t1 = w.clock();
     i32 rst = insert_txn(remote, first, txn_len, np, p0);
-    (void)prof_t0;
+    (void)prof_t0; (void)prof_t1;
+#ifdef CRDT_PROF_TXN2
+    if (prof_mode == 3u) {  // prologue (agent switch, fits, assign_order_to_client) / ops / parents / insert_txn
+      u64 prof_td = w.clock();
+      inc(S_PROF0, (u32)(prof_ta - prof_t0)); inc(S_PROF1, (u32)(prof_tb - prof_ta));
+      inc(S_PROF2, (u32)(prof_t1 - prof_tb)); inc(S_PROF3, (u32)(prof_td - prof_t1));
+    }
+#endif
+#ifdef CRDT_PROF_TXN
+    if (prof_mode == 3u) {
+      u32 tot = (u32)(w.clock() - prof_t0);
+      inc(S_PROF0, tot - pt_scan - pt_del - pt_ins); inc(S_PROF1, pt_scan); inc(S_PROF2, pt_del); inc(S_PROF3, pt_ins);
+    }
+    pt_scan = pt_del = pt_ins = 0;
+#endif
     return rst;
 #else
     return insert_txn(remote, first, txn_len, np, p0);

@@ -132,6 +132,7 @@ struct WaveGPU {
   typedef __attribute__((address_space(3))) u32 lds_u32;  // ds_read/ds_write, never flat
   lds_u32* rt = nullptr;
   lds_u32* rk = nullptr;  // agent ranks (documents with <= RANK_LDS agents)
+  lds_u32* pf = nullptr;  // integrate's scan: the successor leaf, requested ahead (LDS-DMA)
   u32 rcap = 0;
   u32* hrow = nullptr;  // HR: this document's rows (192 u32 each: blk[64], cnt[64], vis[64])
   u32* gsob = nullptr;  // HR: block -> row << 6 | slot
@@ -401,17 +402,28 @@ struct WaveGPU {
   __device__ __forceinline__ u32 rank_of(const AgentRec* agents, u32 n, u32 a) const {
     return n <= RANK_LDS ? uni(rk[a]) : ld(&at(agents, a)->rank);
   }
-  __device__ __forceinline__ u32 scan_batch(u32 a, u32 n, u32 X, u32 orr, u32 my_rank, const u16* oag,
+  // (split in two: the agent gather is issued first, so that loads requested between the two
+  // halves -- the successor leaf -- are in flight while the wave waits for it)
+  __device__ __forceinline__ u32 scan_gather(u32 a, u32 n, const u16* oag) const {
+    u32 l = lane();
+    u32 o = (l >= a && l < n) ? (u32)eo : rdlane(eo, a);  // (lanes outside read a valid order's entry)
+    return *(const u16*)((const char*)oag + (u64)(o * 2u));
+  }
+  // the LDS rank table as one row (lane a: agent a's rank), read before an LDS-DMA is requested:
+  // an LDS read issued after one waits for every outstanding load, the DMA's included
+  __device__ __forceinline__ u32 rank_row(u32 n_agents) const { return n_agents <= RANK_LDS ? (u32)rk[lane()] : 0u; }
+  __device__ __forceinline__ u32 scan_batch(u32 ag, u32 rt, u32 me, u32 a, u32 n, u32 X, u32 orr,
                                             const AgentRec* agents, u32 n_agents, u32 tkey, u32 tlen, u32 tagent, u32& last,
                                             u32& last_scan) const {
     // (the replay's register budget is spent: per-lane values are transient, the per-lane tests
     // become lane masks at once, and the rest is scalar mask arithmetic)
     u32 l = lane();
-    u32 o = (l >= a && l < n) ? (u32)eo : rdlane(eo, a);  // (lanes outside read a valid order's entry)
-    u32 ag = *(const u16*)((const char*)oag + (u64)(o * 2u));
+    u32 o = (l >= a && l < n) ? (u32)eo : rdlane(eo, a);
     ag = o - tkey < tlen ? tagent : ag;  // the client_with_order tail run is not in the map yet
-    u32 rk = n_agents <= RANK_LDS ? (u32)this->rk[ag]  // AgentRec::rank, from LDS when it fits
-                                  : *(const u32*)((const char*)agents + (u64)(ag * (u32)sizeof(AgentRec) + 12u));
+    bool small = n_agents <= RANK_LDS;  // AgentRec::rank from the rank row when it fits (bpermute: no LDS read)
+    u32 my_rank = small ? rdlane(rt, me) : ld(&at(agents, me)->rank);
+    u32 rk = small ? (u32)__builtin_amdgcn_ds_bpermute((int)(ag * 4u), (int)rt)
+                   : *(const u32*)((const char*)agents + (u64)(ag * (u32)sizeof(AgentRec) + 12u));
     u64 lt = ballot(my_rank > rk);
     u64 ev = ballot(eo == orr) | ballot(el != X) | (~lt & ballot(er == orr));
     u64 in = (n >= 64u ? ~0ull : ((1ull << n) - 1ull)) & (~0ull << a);
@@ -489,6 +501,23 @@ struct WaveGPU {
     if (l < (u32)L) *(uint4*)(dst + l) = make_uint4(mo, ml, mr, mn);
   }
   __device__ __forceinline__ void cache_from_moved() { eo = mo; el = ml; er = mr; en = (i32)mn; }
+  // A leaf requested ahead into this wave's LDS row by LDS-DMA (global_load_lds_dwordx4: lane l's
+  // entry to row + 16 l, no VGPR holds it in flight), made the cached leaf once integrate's scan
+  // reaches it (returns its entry count).
+  __device__ __forceinline__ void leaf_prefetch(const Span* p) const {
+    typedef __attribute__((address_space(1))) u32 g_u32;
+    u32 l = lane();
+    if (l < (u32)L) __builtin_amdgcn_global_load_lds((g_u32*)(p + l), pf, 16, 0, 0);
+  }
+  __device__ __forceinline__ u32 cache_from_prefetch() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA counts in vmcnt; it is not a VGPR the compiler tracks)
+    u32 l = lane();
+    bool in = l < (u32)L;
+    const lds_u32* q = pf + 4u * (l & (u32)(L - 1));
+    u32 a = q[0], b = q[1], c = q[2], d = q[3];
+    eo = in ? a : 0u; el = in ? b : 0u; er = in ? c : 0u; en = in ? (i32)d : 0;
+    return __popcll(ballot(en != 0));
+  }
   // lof[order + t] = v for every item of the entries in lanes [a, b): 64 items per step, each
   // lane finding its entry by a binary search over the entries' length prefix (entries sit in
   // lanes < L: log2(L) steps, on bpermute byte addresses), then the item's order from one more
