@@ -8,6 +8,6 @@ if [ -f text-crdt-rust_amd/build/libcrdt_gpu_proftxn2.so ]; then
   PROF_TXN2=1 CRDT_GPU_LIB=text-crdt-rust_amd/build/libcrdt_gpu_proftxn2.so timeout -k 10 300 python scripts/prof_paths.py ${DOCS:-1024} config5 >> $OUT 2>&1 || exit 1
 fi
 if [ -f text-crdt-rust_amd/build/libcrdt_gpu_prof.so ]; then
-  CRDT_GPU_LIB=text-crdt-rust_amd/build/libcrdt_gpu_prof.so timeout -k 10 300 python scripts/prof_paths.py 64 kevin >> $OUT 2>&1 || exit 1
+  KEVIN_OPS=5000000 CRDT_GPU_LIB=text-crdt-rust_amd/build/libcrdt_gpu_prof.so timeout -k 10 300 python scripts/prof_paths.py 4 kevin >> $OUT 2>&1 || exit 1
 fi
 cat $OUT

@@ -18,7 +18,7 @@ e = crdt_amd.Engine(n, 32)
 if mode == "random":  # config 4: 20,000 generated ops per document (bench_config4.py's shape)
     e.stage_random(list(range(n)), "gen", 20000, 0xC0FFEE)
 elif mode == "kevin":  # benches/yjs.rs:51-62 shape: single-char prepends (200,000 per document)
-    k = 200_000
+    k = int(os.environ.get("KEVIN_OPS", "200000"))  # (compact local txns: "generic" = the inserts that split the leaf)
     class T:
         counts = np.ones(k, np.uint32)
         patches = np.zeros((k, 3), np.uint32)
@@ -54,7 +54,10 @@ for i, k in enumerate(names):
     c, calls, tx = view["cycles"][i], view["calls"][i], view["txns"][i]
     print(f"  {k:8s} cycles {c:.4g} ({c / tot:.1%})  calls {calls:.0f}  txns {tx:.0f}  cycles/call {c / max(calls, 1):.0f}  cycles/txn {c / max(tx, 1):.0f}")
 s = np.array([e.debug_state(d) for d in range(3, n, 4 * max(1, n // 256))]).astype(np.float64)[:, P0:P0 + 4].mean(axis=0)
-if mode == "random":
+if mode == "kevin":
+    print(f"  compact local loop cycles by part: split_at {s[0]:.4g}, rest of the splitting inserts {s[1]:.4g}, other fast txns {s[2]:.4g}, "
+          f"next record {s[3]:.4g}")
+elif mode == "random":
     print(f"  generated-op cycles by part: draw + op {s[0]:.4g}, fast path without cursor {s[1]:.4g}, cursor in leaf {s[2]:.4g}, leaf switch (commit + descent + load) {s[3]:.4g}")
 elif os.environ.get("PROF_TXN2"):  # a -DCRDT_PROF_TXN2 build: apply_txn's bookkeeping by part
     print(f"  apply_txn cycles by part: prologue (author switch, fits, assign_order_to_client) {s[0]:.4g}, ops {s[1]:.4g}, "

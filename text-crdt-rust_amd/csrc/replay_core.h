@@ -117,6 +117,7 @@ struct Replayer {
   u32 prof_mode = 0; // document d % 4: 0 cycles, 1 calls, 2 txns per path, 3 detail (below)
   u32 prof_gen = 0;  // generated ops (config 4): detail = gen / fast path / cursor / leaf switch
   u32 prof_cur = 0, prof_sw = 0;  // cycles in cursor_at_content_pos and in its leaf switches
+  u64 prof_t2 = 0;    // (compact local loop detail)
   u32 prof_split = 0;  // cycles in split_at (-DCRDT_PROF_LOOP: detail of fast_deletes' leaf-split loop)
   // -DCRDT_PROF_TXN: apply_txn's cycles by part (txn bookkeeping / integrate's scan / deletes /
   // op fetch + origins + insert_internal), added to the DocState counters of d % 4 == 3 documents
@@ -1936,10 +1937,7 @@ struct Replayer {
   // stops at once and the run cannot be appended: insert_internal (mutations.rs:17-179) splits
   // the entry at the cursor (remainder after the item) and makes room, without a leaf split.
   // Returns 0, having changed nothing, when the leaf or the order map has no room.
-  // front: the cursor is at offset 0 of entry 0 (a local insert at position 0; never remote)
-  // (kf: the length of the front run this txn starts, see leaf_insert_front; returns txns placed)
-  CRDT_HD u32 leaf_insert(u32 idx, u32 off, const Span& item, u32 front, u32 kf) {
-    if (front) return leaf_insert_front(item, kf);
+  CRDT_HD u32 leaf_insert(u32 idx, u32 off, const Span& item) {
     Span e = w.cget(idx);
     u32 n = g(C_N);
     u32 len = (u32)item.len;
@@ -1973,20 +1971,27 @@ struct Replayer {
   // (the item's for j = 0, else prepend j-1's first item; doc.rs:443-453); integrate stops at once
   // and insert_internal puts it at index 0, never prepending it onto entry 0 (orders only grow).
   // So the prepends that fit the leaf are one shift plus one lane-parallel write, newest at lane
-  // 0; the one that finds the leaf full goes the general way (a split at index 0).  Returns the
-  // txns placed (0: no room, nothing changed).
-  CRDT_HD u32 leaf_insert_front(const Span& item, u32 k) {
+  // 0.  The prepend that finds the leaf full is what insert_internal does with an item at index
+  // 0 of a full leaf: split_at(0) moves every entry to a new leaf linked right after it
+  // (mutations.rs:96-121, the cursor does not follow), and the item is entry 0 of the emptied
+  // leaf -- which the next prepends fill again.  So a front run goes on through the splits.
+  // Each chunk is committed as it is placed (fast_txn_commit: the first one's order is
+  // S_NEXT_ORDER).  orr0: the first prepend's origin_right.  Returns the txns placed (0: no room,
+  // nothing changed).
+  // A front run's prepends that fit the cached leaf, committed (fast_txn_commit; the first one's
+  // order is S_NEXT_ORDER).  Returns the txns placed (0: no room, nothing changed).
+  CRDT_HD u32 leaf_insert_front(u32 orr0, u32 len, u32 rem) {
     u32 n = g(C_N);
-    u32 len = (u32)item.len;
     u32 m = (u32)L - n;
-    m = m < k ? m : k;
-    if (m == 0u) return 0;
-    if (g(K_MAP) - item.order < m * len) return 0;
+    m = m < rem ? m : rem;
+    if (m == 0u) return 0u;
+    u32 first = g(S_NEXT_ORDER);
+    if (g(K_MAP) - first < m * len) return 0u;
     w.cache_shift_right(0u, n, m);
     p(C_N, n + m);
     inc(S_N_ENTRIES, m);
-    map_fill(item.order, m * len, g(C_LEAF));  // notify (doc.rs:143-153)
-    u32 top = m - 1u, first = item.order, orr0 = item.orr;
+    map_fill(first, m * len, g(C_LEAF));  // notify (doc.rs:143-153)
+    u32 top = m - 1u;
     w.cset_lanes(0u, m, [&](u32 lane) {
       u32 j = top - lane;
       u32 o = first + j * len;
@@ -1994,6 +1999,7 @@ struct Replayer {
     });
     p(C_NOW, g(C_NOW) + m * len);
     p(C_DIRTY, 1u);
+    fast_txn_commit(first, m * len);
     return m;
   }
   // A local delete of l visible items that starts at offset `off` of visible entry idx of the
@@ -2235,13 +2241,25 @@ struct Replayer {
       if (c.off == el) {
         if (can_append_u(e, item)) return fast_typing(b0, nv, remote, idx, orr, agent, o, first);
       }
+      // a local insert at position 0 (offset 0 only there) may start a front run
+      u32 front = remote ? 0u : (c.off == 0u ? 1u : 0u);
       // no room for the item (+ the entry's remainder): a leaf split, the general path's job
       if (g(C_N) + 1u + (c.off < el) > (u32)L) {
         // integrate stops at once here (checked above), so apply_txn would only insert_internal
         // the item, splitting the leaf (mutations.rs:17-179): do that here when a leaf is free
         if ((g(K_LEAF) - g(S_N_LEAVES) >= 2u) && (g(K_MAP) - first >= l)) {
+#ifdef CRDT_PROF
+          prof_cat = 1u;
+#endif
           insert_items(item, Span{0, 0, 0, 0}, Span{0, 0, 0, 0}, 1u, c, INVALID);
           fast_txn_commit(first, l);
+          // a prepend that split a full leaf at index 0 (insert_internal: split_at(0) moves every
+          // entry to a new leaf linked right after it, the cursor does not follow, mutations.rs:
+          // 96-121) is entry 0 of the emptied leaf: the front run it starts refills it
+          if (front & cpt) {
+            u32 kf = w.front_scan(b0, nv, agent, l);
+            if (kf > 1u) return (1u + leaf_insert_front(first, l, kf - 1u)) * per;
+          }
           return per;
         }
         p(F_PRE, 1u);
@@ -2253,14 +2271,14 @@ struct Replayer {
       u32 total;
       u32 nt = typing_run(b0, nv, remote, agent, (agent & 0xFFFFu) | (o.w1 & 0xFFFF0000u), o, total);
       item.len = (i32)total;
-      // a local insert at position 0 (offset 0 only there) may start a front run
-      u32 front = remote ? 0u : (c.off == 0u ? 1u : 0u);
       u32 kf = (front & cpt) && nt == 1u ? w.front_scan(b0, nv, agent, l) : 1u;
-      u32 r = leaf_insert(idx, c.off, item, front, kf);
-      if (!r) return 0;
-      total += (r - 1u) * l;  // (r > 1 only for a front run, whose first txn is the item: total == l)
+      if (front) {  // (a front run commits itself; with kf > 1, nt == 1)
+        u32 r = leaf_insert_front(item.orr, total, kf);
+        return r ? (nt + r - 1u) * per : 0u;
+      }
+      if (!leaf_insert(idx, c.off, item)) return 0;
       fast_txn_commit(first, total);
-      return (nt + r - 1u) * per;
+      return nt * per;
     }
     i32 el = w.cget_len(idx);
     if (el <= 0) return 0;                // already deleted
@@ -2360,13 +2378,35 @@ struct Replayer {
       } else if (kind == REC_LC) {
         // the same for compact local txns (local-trace corpora: configs 1 and 3)
         while (true) {
+#ifdef CRDT_PROF
+          u64 t0 = w.clock();
+          prof_split = 0u;
           u32 fast = fast_txn(pos, REC_LC, 0u, h, Rec{0, 0, 0, 0});
+          u64 t1 = w.clock();
+          u32 dt = prof_mode == 0u ? (u32)(t1 - t0) : prof_mode == 1u ? 1u : fast;
+          if (prof_mode != 3u && fast) {  // (1: an insert that splits the leaf)
+            if (prof_cat == 0u) inc(S_PROF0, dt);
+            else if (prof_cat == 1u) inc(S_PROF1, dt);
+            else if (prof_cat == 2u) inc(S_PROF2, dt);
+            else inc(S_PROF3, dt);
+          }
+          if (prof_mode == 3u && fast) {  // detail: split_at / the rest of a splitting insert / other fast txns / the loop
+            if (prof_cat == 1u) { inc(S_PROF0, prof_split); inc(S_PROF1, (u32)(t1 - t0) - prof_split); }
+            else inc(S_PROF2, (u32)(t1 - t0));
+            prof_t2 = t1;
+          }
+#else
+          u32 fast = fast_txn(pos, REC_LC, 0u, h, Rec{0, 0, 0, 0});
+#endif
           if (!fast) break;
           pos += fast;
           if (pos >= rn) break;
           w.x_pin();
           h = rec(pos);
           kind = rec_kind(h);
+#ifdef CRDT_PROF
+          if (prof_mode == 3u) inc(S_PROF3, (u32)(w.clock() - prof_t2));
+#endif
           if (kind != REC_LC) break;
         }
         if (pos >= rn) break;
