@@ -22,6 +22,7 @@ struct EmuDoc {
   std::vector<Span> leaves;
   std::vector<u32> dir_leaf, dir_vis, sol, leaf_of, parents, frontier;
   std::vector<u16> agent_of;
+  std::vector<u32> leaf_agents;
   std::vector<CwoRun> cwo;
   std::vector<ARun> arun;
   std::vector<DelRun> dels;
@@ -44,6 +45,7 @@ struct EmuDoc {
     p.slot_of_leaf = sol.data();
     p.leaf_of = leaf_of.data();
     p.agent_of = agent_of.data();
+    p.leaf_agents = leaf_agents.data();
     p.cwo = cwo.data();
     p.arun = arun.data();
     p.dels = dels.data();
@@ -70,6 +72,8 @@ struct EmuDoc {
     dir_vis.assign((size_t)c.blk * GROUP, 0);
     leaf_of.assign(std::max<u32>(c.map, 1), 0xDEADBEEFu);
     agent_of.assign(std::max<u32>(c.map, 1), 0xBEEFu);
+    leaf_agents.assign((size_t)c.leaf * lag_words(L), 0xDEADBEEFu);  // (garbage but word 0: rows are stale until written)
+    for (size_t k = 0; k < leaf_agents.size(); k += lag_words(L)) leaf_agents[k] = 0;
     cwo.assign(c.cwo, CwoRun{});
     arun.assign(c.arun, ARun{});
     dels.assign(c.del, DelRun{});
@@ -104,6 +108,7 @@ struct EmuDoc {
   void grow(u32 need) {
     grow_events++;
     grow_mask |= need;
+    leaf_agents.assign((size_t)seg.leaf_cap * 2 * lag_words(L), 0u);  // (the engine's relayout: every row stale)
     if (need & 1u) {
       u32 nl = seg.leaf_cap * 2 > MAX_LEAVES ? MAX_LEAVES : seg.leaf_cap * 2;
       leaves.resize((size_t)nl * L, Span{0, 0, 0, 0});

@@ -127,7 +127,33 @@ struct WaveCPU {
   void rank_load(const AgentRec*, u32) const {}
   u32 rank_of(const AgentRec* agents, u32, u32 a) const { return agents[a].rank; }
   mutable const u16* oag = nullptr;  // (scan_gather's map, read by scan_batch)
-  u32 scan_gather(u32, u32, const u16* m) const { oag = m; return 0u; }
+  u32 scan_gather(u32, const u16* m) const { oag = m; return 0u; }
+  // agent rows: word 0 (valid) is what the replay sees; a current row must hold exactly the map's
+  // agents of the cached leaf's entries (checked here: a stale row taken as current aborts)
+  mutable const u32* lag_p = nullptr;
+  u32 lag_ld(const u32* p) const { lag_p = p; return p[0]; }
+  u32 lag_valid(u32 lw) const { return lw == 1u; }
+  u32 lag_agents(u32, u32 n, const u16* m, u32 tkey, u32 tlen, u32 tagent) const {
+    oag = m;
+    for (u32 j = 0; j < n; j++) {
+      u32 o = c[j].order, want = o - tkey < tlen ? tagent : m[o];
+      u32 v = lag_p[lag_words(L) / 2 + j / 2];
+      u32 got = (j & 1) ? v >> 16 : v & 0xFFFFu;
+      if (got != want) {
+        std::fprintf(stderr, "wave_cpu: stale leaf agent row (entry %u: %u, map %u)\n", j, got, want);
+        std::abort();
+      }
+    }
+    return 0u;
+  }
+  void lag_store(u32* p, u32, u32 n, u32 tkey, u32 tlen, u32 tagent) const {
+    for (u32 j = 0; j < (u32)L / 2; j++) p[lag_words(L) / 2 + j] = 0;
+    for (u32 j = 0; j < n; j++) {
+      u32 o = c[j].order, a = (o - tkey < tlen ? tagent : oag[o]) & 0xFFFFu;
+      p[lag_words(L) / 2 + j / 2] |= (j & 1) ? a << 16 : a;
+    }
+    p[0] = 1u;
+  }
   u32 rank_row(u32) const { return 0u; }
   u32 scan_batch(u32, u32, u32 me, u32 a, u32 n, u32 X, u32 orr, const AgentRec* agents, u32 n_agents, u32 tkey,
                  u32 tlen, u32 tagent, u32& last, u32& last_scan) const {

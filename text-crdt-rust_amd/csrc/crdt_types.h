@@ -276,6 +276,11 @@ struct DocState {
   u32 prof0, prof1, prof2, prof3;  // diagnostic cycle counters (-DCRDT_PROF builds only)
 };
 
+// Per-leaf cache of the agents of the leaf's entries (read by DOC_TRACK_AGENT documents): word 0 = 1 when
+// the row is current, words [lag_words/2, +L/2) = the agent of entry j's first order (u16, two
+// per word).  integrate's scan reads one row per leaf instead of one order -> agent map line per
+// entry; a commit of the leaf (or its creation) clears word 0, the scan rewrites a stale row.
+constexpr u32 lag_words(int L) { return L >= 16 ? (u32)L : 16u; }
 struct Pools {
   Span* leaves;        // [leaf][L]
   u32* dir_leaf;       // [blk*64 + i]
@@ -283,6 +288,7 @@ struct Pools {
   u32* slot_of_leaf;   // [2 * (leaf_base + leaf)] = blk<<6 | i, [+1] = successor leaf (END_LEAF: last)
   u32* leaf_of;        // [map_base + order]
   u16* agent_of;       // [map_base + order] (DOC_TRACK_AGENT documents)
+  u32* leaf_agents;    // [(leaf_base + leaf) * lag_words(L)]: integrate's scan cache, see lag_words
   CwoRun* cwo;
   ARun* arun;
   DelRun* dels;

@@ -68,6 +68,7 @@ struct PoolSet {
   u32* dir_vis = nullptr;
   u32* leaf_of = nullptr;
   u16* agent_of = nullptr;  // (allocated for every map slot when some document keeps it)
+  u32* lag = nullptr;       // leaf agent rows (crdt_types.h lag_words; every leaf slot)
   u32* hrows = nullptr;     // two-level root rows (documents past the LDS root)
   u32* gsob = nullptr;      // their blocks' row slots (every block slot when some document needs it)
   CwoRun* cwo = nullptr;
@@ -82,7 +83,7 @@ struct PoolSet {
   AgentRec* agents = nullptr;
   u64 bytes = 0;
   void free_all() {
-    dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(agent_of); dfree(hrows); dfree(gsob); dfree(cwo); dfree(arun);
+    dfree(leaves); dfree(sol); dfree(dir_leaf); dfree(dir_vis); dfree(leaf_of); dfree(agent_of); dfree(lag); dfree(hrows); dfree(gsob); dfree(cwo); dfree(arun);
     dfree(dels); dfree(dd); dfree(ddb); dfree(txns); dfree(parents); dfree(frontier); dfree(groups); dfree(agents);
     bytes = 0;
   }
@@ -237,6 +238,7 @@ struct crdt_engine {
     p.slot_of_leaf = ps.sol;
     p.leaf_of = ps.leaf_of;
     p.agent_of = ps.agent_of;
+    p.leaf_agents = ps.lag;
     p.hrows = ps.hrows;
     p.gsob = ps.gsob;
     p.cwo = ps.cwo;
@@ -383,8 +385,9 @@ struct crdt_engine {
       nseg[d] = s;
     }
     // sizes of the new pools (element counts; 0 -> one element)
+    const u64 n_lag = nl * lag_words(L);
     const u64 n_agent_of = any_agent_map ? nm : 1, n_hrows = any_hroot ? nhr * HROOT_ROW : 1, n_gsob = any_hroot ? nb : 1;
-    np.bytes = nl * L * 16 + nl * 8 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) +
+    np.bytes = nl * L * 16 + nl * 8 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) + nl * lag_words(L) * 4 +
                (any_hroot ? nhr * HROOT_ROW * 4 + nb * 4 : 0) + nc * 16 + na * 16 + ndl * 12 +
                ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * (u64)sizeof(AgentRec) + nfr * 4 + nb * 16;
     if (getenv("CRDT_DEBUG_MEM"))
@@ -426,6 +429,8 @@ struct crdt_engine {
     if (!r) r = step(pools.dir_vis, np.dir_vis, nb * GROUP, RL_DIR_VIS);
     if (!r) r = step(pools.leaf_of, np.leaf_of, nm, RL_LEAF_OF);
     if (!r) r = step(pools.agent_of, np.agent_of, n_agent_of, RL_AGENT_OF);
+    if (!r) r = step(pools.lag, np.lag, n_lag, RL_N);  // (not moved: every row starts stale)
+    if (!r) HIPCHK(hipMemsetAsync(pools.lag, 0, n_lag * 4, stream));
     if (!r) r = step(pools.hrows, np.hrows, n_hrows, RL_N);  // (rebuilt from the groups at every launch)
     if (!r) r = step(pools.gsob, np.gsob, n_gsob, RL_N);
     if (!r) r = step(pools.cwo, np.cwo, nc, RL_CWO);

@@ -58,6 +58,7 @@ enum : u32 {
   K_FR,                   // frontier capacity
   P_OAG,                  // (2 slots) order -> agent map
   K_AGMAP = P_OAG + 2,    // 1: the document keeps the order -> agent map (DOC_TRACK_AGENT)
+  P_LAG,                  // (2 slots) leaf agent rows (crdt_types.h lag_words)
   // x1: DocState, field for field (struct order), then the per-call flags
   S_BASE = 64,
   S_STATUS = 64, S_REC_POS, S_N_LEAVES, S_N_BLOCKS, S_NG, S_NEXT_ORDER, S_LEN, S_N_CWO, S_N_DEL,
@@ -91,7 +92,7 @@ enum : u32 {
   T_OA_ID, T_OA_BASE, T_OA_CNT,
   N_SLOTS
 };
-static_assert(K_AGMAP < 64, "read-only slots live in the first context register");
+static_assert(P_LAG + 1 < 64, "read-only slots live in the first context register");
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
 static_assert(F_BASE < 128, "DocState and the flags live in the second context register");
 static_assert(N_SLOTS <= 192, "three context registers");
@@ -141,6 +142,10 @@ struct Replayer {
   CRDT_HD u32* sol() const { return ptr<u32>(P_SOL); }
   CRDT_HD u32* lof() const { return ptr<u32>(P_LOF); }
   CRDT_HD u16* oag() const { return ptr<u16>(P_OAG); }
+  CRDT_HD u32* lagp(u32 leaf) const { return w.template at<lag_words(L)>(ptr<u32>(P_LAG), leaf); }
+  // a leaf's agent row is no longer current (its entries change, or it is new).  (Every document
+  // has the rows: a store cheaper in registers than a test of K_AGMAP at every commit.)
+  CRDT_HD void lag_stale(u32 leaf) { w.st(lagp(leaf), 0u); }
   CRDT_HD CwoRun* cwo() const { return ptr<CwoRun>(P_CWO); }
   CRDT_HD ARun* arun() const { return ptr<ARun>(P_ARUN); }
   CRDT_HD DelRun* dels() const { return ptr<DelRun>(P_DELS); }
@@ -168,6 +173,7 @@ struct Replayer {
     pset(P_SOL, P.slot_of_leaf + 2u * sg.leaf_base);  // {slot, successor} per leaf
     pset(P_LOF, P.leaf_of + sg.map_base);
     pset(P_OAG, P.agent_of + sg.map_base);
+    pset(P_LAG, P.leaf_agents + sg.leaf_base * (u64)lag_words(L));
     pset(P_CWO, P.cwo + sg.cwo_base);
     pset(P_ARUN, P.arun + sg.arun_base);
     pset(P_DELS, P.dels + sg.del_base);
@@ -237,6 +243,7 @@ struct Replayer {
     p(S_GEN_DONE, 0);
     p(S_N_DDB, 0);
     w.zero_leaf(leafp(0), L);
+    lag_stale(0u);
     w.st(dl(), 0u);
     w.st(dv(), 0u);
     w.st(sol(), 0u);
@@ -382,6 +389,7 @@ struct Replayer {
     if (lf == INVALID) return;
     if (!g(C_DIRTY)) return;
     w.cache_store(leafp(lf));
+    lag_stale(lf);
     dir_set_cached_vis(g(C_NOW));
     p(C_DIRTY, 0);
   }
@@ -641,6 +649,7 @@ struct Replayer {
     u32 stolen = w.cache_vis_from(idx);
     u32 first_moved = w.cget_order(idx);
     w.cache_write_moved(leafp(nl), idx, n, padding);
+    lag_stale(nl);
     if (tracked()) w.fill_runs(lof(), idx, n, nl);  // notify every moved entry
     w.cache_clear(idx, n);
     p(C_NOW, g(C_NOW) - stolen);
@@ -1281,10 +1290,23 @@ struct Replayer {
               CRDT_STAT(45, 1); CRDT_STAT(46, nn - c.idx);
               // (the successor leaf is requested before this leaf is evaluated: a scan that runs
               // through it finds it in LDS)
-              u32 ag = w.scan_gather(c.idx, nn, oag());
+              // the agents of the leaf's entries: its agent row when current (a leaf with
+              // uncommitted changes has none), else gathered from the order -> agent map and
+              // written as its row
+              u32 clean = g(C_DIRTY) ^ 1u;
+              u32 lw = 0u;
+              if (clean) lw = w.lag_ld(lagp(c.leaf));
               u32 rt = w.rank_row(na);
               u32 pslot, psucc;
               u32 pl = prefetch_succ(pslot, psucc);
+              u32 ag;
+              CRDT_STAT(55, clean); CRDT_STAT(56, clean && w.lag_valid(lw));
+              if (clean && w.lag_valid(lw)) {
+                ag = w.lag_agents(lw, nn, oag(), g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT));
+              } else {
+                ag = w.scan_gather(nn, oag());
+                if (clean) w.lag_store(lagp(c.leaf), ag, nn, g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT));
+              }
               u32 f = w.scan_batch(ag, rt, agent, c.idx, nn, item.ol, item.orr, agents(), na,
                                    g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT), last, last_scan);
               if (last != INVALID) {

@@ -402,12 +402,35 @@ struct WaveGPU {
   __device__ __forceinline__ u32 rank_of(const AgentRec* agents, u32 n, u32 a) const {
     return n <= RANK_LDS ? uni(rk[a]) : ld(&at(agents, a)->rank);
   }
-  // (split in two: the agent gather is issued first, so that loads requested between the two
-  // halves -- the successor leaf -- are in flight while the wave waits for it)
-  __device__ __forceinline__ u32 scan_gather(u32 a, u32 n, const u16* oag) const {
+  // the agents of the cached leaf's entries [0, n) from the order -> agent map (lanes >= n read
+  // entry 0's)
+  __device__ __forceinline__ u32 scan_gather(u32 n, const u16* oag) const {
     u32 l = lane();
-    u32 o = (l >= a && l < n) ? (u32)eo : rdlane(eo, a);  // (lanes outside read a valid order's entry)
+    u32 o = l < n ? (u32)eo : rdlane(eo, 0);
     return *(const u16*)((const char*)oag + (u64)(o * 2u));
+  }
+  // A leaf's agent row (crdt_types.h lag_words): one word per lane ...
+  __device__ __forceinline__ u32 lag_ld(const u32* p) const {
+    u32 l = lane();
+    return l < lag_words(L) ? *(const u32*)(p + l) : 0u;
+  }
+  __device__ __forceinline__ u32 lag_valid(u32 lw) const { return rdlane(lw, 0) == 1u; }
+  // ... entry l's agent from it ...
+  __device__ __forceinline__ u32 lag_agents(u32 lw, u32 n, const u16* oag, u32 tkey, u32 tlen, u32 tagent) const {
+    (void)n; (void)oag; (void)tkey; (void)tlen; (void)tagent;
+    u32 l = lane();
+    u32 v = shfl(lw, lag_words(L) / 2u + (l >> 1));
+    return (l & 1u) ? v >> 16 : v & 0xFFFFu;
+  }
+  // ... and written from the gathered agents (the client_with_order tail run's orders are not in
+  // the map yet: their agent is the tail's), with word 0 = 1
+  __device__ __forceinline__ void lag_store(u32* p, u32 ag, u32 n, u32 tkey, u32 tlen, u32 tagent) const {
+    u32 l = lane();
+    u32 o = l < n ? (u32)eo : rdlane(eo, 0);
+    ag = o - tkey < tlen ? tagent : ag;
+    u32 lo = shfl(ag, 2u * (l - lag_words(L) / 2u)), hi = shfl(ag, 2u * (l - lag_words(L) / 2u) + 1u);
+    u32 v = l == 0u ? 1u : ((hi << 16) | (lo & 0xFFFFu));
+    if (l == 0u || (l >= lag_words(L) / 2u && l < lag_words(L) / 2u + (u32)L / 2u)) *(u32*)(p + l) = v;
   }
   // the LDS rank table as one row (lane a: agent a's rank), read before an LDS-DMA is requested:
   // an LDS read issued after one waits for every outstanding load, the DMA's included
