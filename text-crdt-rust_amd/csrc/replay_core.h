@@ -2504,6 +2504,9 @@ struct Replayer {
         // compact remote txns (the remote-batch hot path) get their own instance of the fast paths,
         // with record kind, format and stride known at compile time
         // (also the compact local form and generated ops: the other batch shapes)
+        // (a general remote txn by another author than the cached one, or with several frontier
+        // heads, fails fast_txn_ok at once: skip the attempt's record decoding)
+        if (kind == REC_RTXN) tried |= (((h.w1 & 0xFFFFu) != g(T_AG_ID)) | (g(S_N_FR) != 1u)) ? 1u : 0u;
         u32 fast = tried ? 0u : fast_txn(pos, kind, 0u, h, gop);  // (a GEN record was tried above)
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
