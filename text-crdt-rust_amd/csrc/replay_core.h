@@ -90,6 +90,10 @@ enum : u32 {
   // the last non-author agent seq_to_order looked up: its item_orders runs (base, count).  Valid
   // while that agent authors nothing (use_agent drops it when it becomes the author).
   T_OA_ID, T_OA_BASE, T_OA_CNT,
+  // the author's item_orders run before its tail (a txn that starts a run retires the tail to
+  // it): a remote txn's parent is usually its author's previous item, which is there.  Valid
+  // while the author stays (use_agent clears it; T_AGP_LEN = 0: none)
+  T_AGP_KEY, T_AGP_ORDER, T_AGP_LEN,
   N_SLOTS
 };
 static_assert(P_LAG + 1 < 64, "read-only slots live in the first context register");
@@ -213,7 +217,7 @@ struct Replayer {
     p(T_TX_ORDER, 0); p(T_TX_LEN, 0); p(T_TX_SHADOW, 0);
     p(T_FR0, ROOT_ORDER);
     p(T_AG_ID, INVALID); p(T_AG_BASE, 0); p(T_AG_CNT, 0); p(T_AG_CAP, 0);
-    p(T_AGL_KEY, 0); p(T_AGL_ORDER, 0); p(T_AGL_LEN, 0);
+    p(T_AGL_KEY, 0); p(T_AGL_ORDER, 0); p(T_AGL_LEN, 0); p(T_AGP_LEN, 0);
     p(T_OA_ID, INVALID); p(T_OA_BASE, 0); p(T_OA_CNT, 0);
     p(T_RB_BASE, 0x80000000u);  // pos - rb_base >= 64 for every valid pos
     p(F_FAST, 0);
@@ -795,6 +799,7 @@ struct Replayer {
     if (a == g(T_OA_ID)) p(T_OA_ID, INVALID);  // (its run count changes from now on)
     flush_agent();
     p(T_AG_ID, a);
+    p(T_AGP_LEN, 0);
     AgentRec r = w.ld_agent(w.at(agents(), a));  // (with the copy of its last run: no second load)
     p(T_AG_BASE, r.run_base);
     p(T_AG_CNT, r.run_cnt);
@@ -817,6 +822,11 @@ struct Replayer {
         order = g(T_AGL_ORDER) + (seq - key);
         return true;
       }
+      u32 pk = g(T_AGP_KEY);
+      if (seq - pk < g(T_AGP_LEN)) {  // the run before the tail
+        order = g(T_AGP_ORDER) + (seq - pk);
+        return true;
+      }
       base = g(T_AG_BASE);
       cnt = g(T_AG_CNT);
     } else if (agent == g(T_OA_ID)) {
@@ -827,6 +837,12 @@ struct Replayer {
       base = A.run_base;
       cnt = A.run_cnt;
       p(T_OA_ID, agent); p(T_OA_BASE, base); p(T_OA_CNT, cnt);
+      // its last run, copied in its record (current: only its own txns change it, and use_agent
+      // writes the copy back when it stops being the author)
+      if ((cnt != 0u) & (seq - A.tkey < A.tlen)) {
+        order = A.torder + (seq - A.tkey);
+        return true;
+      }
     }
     ARun r;
     if (w.search_run(arun() + base, cnt, seq, r) < 0) return false;
@@ -886,7 +902,10 @@ struct Replayer {
     if (an > 0 && seq == lk + ll && order == g(T_AGL_ORDER) + ll) {
       p(T_AGL_LEN, ll + len);
     } else {
-      if (an) w.st(&w.at(arun(), base + an - 1)->len, ll);
+      if (an) {
+        w.st(&w.at(arun(), base + an - 1)->len, ll);
+        p(T_AGP_KEY, lk); p(T_AGP_ORDER, g(T_AGL_ORDER)); p(T_AGP_LEN, ll);
+      }
       p(T_AGL_KEY, seq); p(T_AGL_ORDER, order); p(T_AGL_LEN, len);
       w.st_arun(w.at(arun(), base + an), ARun{seq, order, len, 0});
       p(T_AG_CNT, an + 1);
