@@ -94,6 +94,8 @@ enum : u32 {
   // it): a remote txn's parent is usually its author's previous item, which is there.  Valid
   // while the author stays (use_agent clears it; T_AGP_LEN = 0: none)
   T_AGP_KEY, T_AGP_ORDER, T_AGP_LEN,
+  // ... and that non-author agent's last run (its record's copy; T_OA_LEN = 0: none)
+  T_OA_KEY, T_OA_ORDER, T_OA_LEN,
   N_SLOTS
 };
 static_assert(P_LAG + 1 < 64, "read-only slots live in the first context register");
@@ -830,6 +832,11 @@ struct Replayer {
       base = g(T_AG_BASE);
       cnt = g(T_AG_CNT);
     } else if (agent == g(T_OA_ID)) {
+      u32 ok_ = g(T_OA_KEY);
+      if (seq - ok_ < g(T_OA_LEN)) {
+        order = g(T_OA_ORDER) + (seq - ok_);
+        return true;
+      }
       base = g(T_OA_BASE);
       cnt = g(T_OA_CNT);
     } else {
@@ -839,7 +846,9 @@ struct Replayer {
       p(T_OA_ID, agent); p(T_OA_BASE, base); p(T_OA_CNT, cnt);
       // its last run, copied in its record (current: only its own txns change it, and use_agent
       // writes the copy back when it stops being the author)
-      if ((cnt != 0u) & (seq - A.tkey < A.tlen)) {
+      u32 tl = cnt != 0u ? A.tlen : 0u;
+      p(T_OA_KEY, A.tkey); p(T_OA_ORDER, A.torder); p(T_OA_LEN, tl);
+      if (seq - A.tkey < tl) {
         order = A.torder + (seq - A.tkey);
         return true;
       }
