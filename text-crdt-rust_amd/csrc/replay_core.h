@@ -1300,6 +1300,7 @@ struct Replayer {
         Cursor left = c, scan_start = c;
         bool scanning = false;
         u32 first_step = 1;
+        u32 tk_ = g(T_CWO_KEY), tl_ = g(T_CWO_LEN), ta_ = g(T_CWO_AGENT);  // (fixed while integrate scans)
         while (true) {
           // From the second step on the cursor sits at the start of an entry of the cached leaf
           // (next_entry), so the entry's item is its first order and its origin_left is the
@@ -1330,13 +1331,13 @@ struct Replayer {
               u32 ag;
               CRDT_STAT(55, clean); CRDT_STAT(56, clean && w.lag_valid(lw));
               if (clean && w.lag_valid(lw)) {
-                ag = w.lag_agents(lw, nn, oag(), g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT));
+                ag = w.lag_agents(lw, nn, oag(), tk_, tl_, ta_);
               } else {
                 ag = w.scan_gather(nn, oag());
-                if (clean) w.lag_store(lagp(c.leaf), ag, nn, g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT));
+                if (clean) w.lag_store(lagp(c.leaf), ag, nn, tk_, tl_, ta_);
               }
               u32 f = w.scan_batch(ag, rt, agent, c.idx, nn, item.ol, item.orr, agents(), na,
-                                   g(T_CWO_KEY), g(T_CWO_LEN), g(T_CWO_AGENT), last, last_scan);
+                                   tk_, tl_, ta_, last, last_scan);
               if (last != INVALID) {
                 scanning = last_scan != 0u;
                 if (last_scan) scan_start = Cursor{c.leaf, last, 0u};
