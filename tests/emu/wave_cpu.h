@@ -43,6 +43,7 @@ struct WaveCPU {
   static u32 uni_(u32 x) { return x; }
   void st(u32* p, u32 v) const { *p = v; }
   void st(i32* p, i32 v) const { *p = v; }
+  void st_lanes(u32* p, u32 v, u32 n) const { if (n) *p = v; }
   template <class T> T ldT(const T* p) const { return *p; }
   template <class T> void stT(T* p, const T& v) const { *p = v; }
   AgentRec ld_agent(const AgentRec* p) const { return *p; }

@@ -150,8 +150,9 @@ struct Replayer {
   CRDT_HD u16* oag() const { return ptr<u16>(P_OAG); }
   CRDT_HD u32* lagp(u32 leaf) const { return w.template at<lag_words(L)>(ptr<u32>(P_LAG), leaf); }
   // a leaf's agent row is no longer current (its entries change, or it is new).  (Every document
-  // has the rows: a store cheaper in registers than a test of K_AGMAP at every commit.)
-  CRDT_HD void lag_stale(u32 leaf) { w.st(lagp(leaf), 0u); }
+  // has the rows; only documents that read them store: a lane predicate, where a branch on
+  // K_AGMAP at every commit cost the register budget.)
+  CRDT_HD void lag_stale(u32 leaf) { w.st_lanes(lagp(leaf), 0u, g(K_AGMAP)); }
   CRDT_HD CwoRun* cwo() const { return ptr<CwoRun>(P_CWO); }
   CRDT_HD ARun* arun() const { return ptr<ARun>(P_ARUN); }
   CRDT_HD DelRun* dels() const { return ptr<DelRun>(P_DELS); }

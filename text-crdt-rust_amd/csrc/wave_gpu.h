@@ -158,6 +158,8 @@ struct WaveGPU {
   __device__ __forceinline__ static u32 uni_(u32 x) { return uni(x); }
   __device__ __forceinline__ void st(u32* p, u32 v) const { *(u32*)p = v; }
   __device__ __forceinline__ void st(i32* p, i32 v) const { *(i32*)p = v; }
+  // the store by lanes [0, n) (n in {0, 1}: a predicated store of one word)
+  __device__ __forceinline__ void st_lanes(u32* p, u32 v, u32 n) const { if (lane() < n) *(u32*)p = v; }
   template <class T> __device__ __forceinline__ T ldT(const T* p) const {
     T t;
     const u32* s = (const u32*)p;
