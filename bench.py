@@ -8,6 +8,14 @@ ListCRDT::new(), replay every document's 259,778 remote ops (merge: (agent,seq)-
 integrate + deletes), rebuild the flat position index (publish), and answer `--queries` pos->loc
 and loc->pos queries per document.  Inputs are staged in HBM before timing.
 
+`--workload config4` (BASELINE config 4, the north star's >= 1 M-document corpus): `--corpus-docs`
+(default 1,000,000) random-edit documents of `--gen-ops` ops each, generated inside the replay wave
+(make_random_change semantics, /root/reference/src/list/doc.rs:544-569).  The corpus is document-
+sharded over the ranks (125,000 documents per rank at N = 8); a rank replays its share in resident
+batches of up to `--batch-docs` documents on one engine (8 batches at N = 1).  One step = the whole
+corpus: per batch, the generator seeds of its documents are set on the device, then reset +
+replay + publish, and the digests are copied out on the device.  `value` = corpus ops / step time.
+
 Multi-GPU: one process per GPU.  `--gpus N` with N > 1 started by hand spawns the N
 ranks through torch.distributed.run (the parent never touches a GPU); under torchrun the ranks
 read RANK / LOCAL_RANK / WORLD_SIZE.  The global corpus is N x `--docs` documents, sharded into
@@ -246,18 +254,22 @@ def golden_seq_pos(trace: str):
 
 
 TRAFFIC_WORKLOAD = {"k_replay": "automerge-paper remote, one clean launch",
-                    "k_materialize": "automerge-paper remote, per-document content copies, one launch"}
+                    "k_materialize": "automerge-paper remote, per-document content copies, one launch",
+                    "k_replay:config4": "config 4: generated random edits (20,000 ops/doc), one clean launch",
+                    "k_replay:config3": "config 3: mixed local corpus, shared record streams, one clean launch",
+                    "k_replay:config3_noshare": "config 3: mixed local corpus, per-document record streams, one clean launch",
+                    "k_replay:config5": "config 5: concurrent histories (1 M-char base, 16 agents), one clean launch"}
 
 
-def measured_traffic(n_docs: int, kernel: str = "k_replay"):
+def measured_traffic(n_docs: int, kernel: str = "k_replay", workload: str = None):
     """HBM bytes per launch of `kernel` from the committed PMC pass (profiles/traffic_<kernel>.json:
     FETCH_SIZE x 2 + WRITE_SIZE per the MI355X guide's gfx950 correction).  Only a pass of this
     exact workload (TRAFFIC_WORKLOAD) at this document count is reported; anything else is None
     (a pass over another workload says nothing about this launch)."""
-    p = os.path.join(ROOT, "profiles", f"traffic_{kernel}.json")
+    p = os.path.join(ROOT, "profiles", f"traffic_{kernel}{'_' + workload if workload else ''}.json")
     try:
         t = json.load(open(p))
-        if t.get("workload") != TRAFFIC_WORKLOAD.get(kernel) or int(t["docs"]) != n_docs:
+        if t.get("workload") != TRAFFIC_WORKLOAD.get(kernel + (":" + workload if workload else "")) or int(t["docs"]) != n_docs:
             return None
         return t["hbm_bytes_per_launch"]
     except (OSError, KeyError, ValueError):
@@ -389,6 +401,191 @@ def rehearse_cpu(args, world, rank, dist):
 
 
 # ------------------------------------------------------------------------------------------------
+# config 4: the 1 M-document random-edit corpus
+# ------------------------------------------------------------------------------------------------
+def config4_batches(lo: int, n: int, batch_docs: int):
+    """A rank's documents [lo, lo+n) as resident batches of equal size B (the engine's document
+    count): [(first global id, documents of the corpus in it)]; the last batch may hold fewer."""
+    nb = max(1, -(-n // batch_docs))
+    B = -(-n // nb)
+    return B, [(lo + k * B, min(B, n - k * B)) for k in range(nb)]
+
+
+def config4_rehearsal_digest(ids: np.ndarray) -> np.ndarray:
+    """--rehearse-cpu stand-in for a document's digest: a hash of its global id (the rehearsal checks
+    that the shards and the gather cover every corpus document exactly once, in order)."""
+    x = ids.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def cpu_baseline_random(args, threads: int, target_s: float):
+    """Config 4 on host cores: the oracle (reference B-tree restatement, SplitList order index)
+    replays generated documents 0.. of the corpus, one document per task."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+    from oracle_lib import lib as olib
+
+    def run(k):
+        seeds = np.array([splitmix64(args.seed ^ d) & 0xFFFFFFFF for d in range(k)], np.uint32)
+        ck = C.c_uint64()
+        return olib().orc_cpu_baseline_random(k, threads, args.gen_ops, seeds.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                              C.byref(ck), 1)
+    return sampled(run, threads, target_s, 1 << 20)
+
+
+def oracle_digests_random(args, ids, threads: int):
+    """The oracle's digests of corpus documents `ids` (the checker; test infrastructure)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle_lib import OracleDoc
+
+    def one(d):
+        o = OracleDoc(32, 16, split_index=True)
+        assert o.apply_random(o.agent("gen"), args.gen_ops, splitmix64(args.seed ^ int(d)) & 0xFFFFFFFF) == 0
+        return o.digest()
+    with ThreadPoolExecutor(threads) as ex:
+        return np.array(list(ex.map(one, ids)), np.uint64)
+
+
+def run_config4(args, world: int, rank: int, gpu: int, dist):
+    """BASELINE config 4: the corpus sharded over ranks, each rank's share replayed
+    in resident batches on one engine.  Prints the bench line on rank 0."""
+    import ctypes as C
+    import torch
+    D = args.corpus_docs
+    lo, n = shard_balanced(np.ones(D), world, rank)
+    B, batches = config4_batches(lo, n, args.batch_docs)
+    if args.rehearse_cpu:
+        t0 = time.perf_counter()
+        dg = np.concatenate([config4_rehearsal_digest(np.arange(b0, b0 + m, dtype=np.uint64)) for b0, m in batches])
+        t_max, per_rank, all_dg = reduce_over_ranks(time.perf_counter() - t0, dg, dist, torch.device("cpu"))
+        if rank == 0:
+            want = config4_rehearsal_digest(np.arange(D, dtype=np.uint64))
+            print(json.dumps({"rehearsal": "cpu-gloo", "workload": "config4", "n_gpus": world,
+                              "world_size": dist.get_world_size() if dist else 1, "corpus_docs": D,
+                              "docs_total": int(all_dg.shape[0]), "batch_docs": B,
+                              "shards": [list(shard_balanced(np.ones(D), world, r)) for r in range(world)],
+                              "batches_per_rank": len(batches),
+                              "parity_ok": bool(all_dg.shape[0] == D and (all_dg == want).all()), "value": None}))
+        return
+    import crdt_amd
+    eng = crdt_amd.Engine(B, 32, device=gpu)
+    t0 = time.time()
+    eng.stage_random(list(range(B)), "gen", args.gen_ops, args.seed)
+    dev = torch.device("cuda", gpu)
+    d_dg = torch.zeros(len(batches) * B, dtype=torch.int64, device=dev)
+    canon = np.zeros(len(batches), np.int64)
+    # untimed pass over every batch: capacity growth, then each batch's fitted capacities noted;
+    # the engine is then laid out for the maximum over the batches (crdt_fit_note)
+    for k, (b0, m) in enumerate(batches):
+        eng.reseed_random_async(args.seed, b0)
+        eng.reset_async()
+        st = eng.run()
+        assert (st == 0).all(), np.unique(st)
+        eng.publish_async()
+        eng.sync()
+        canon[k] = int(eng.canon_counts()[:m].astype(np.int64).sum())
+        eng.fit_note(False)
+    eng.fit_note(True)
+    stage_s = time.time() - t0
+    mem = eng.mem_bytes()
+    hip = C.CDLL("libamdhip64.so")
+    ev = [C.c_void_p() for _ in range(2)]
+    for e_ in ev:
+        hip.hipEventCreate(C.byref(e_))
+    s_ = C.c_void_p(eng.stream())
+
+    def step(ms):
+        for k, (b0, m) in enumerate(batches):
+            eng.reseed_random_async(args.seed, b0)
+            eng.reset_async()
+            hip.hipEventRecord(ev[0], s_)
+            eng.run_async()
+            hip.hipEventRecord(ev[1], s_)
+            eng.publish_async()
+            eng.digests_dev_async(d_dg.data_ptr() + 8 * k * B)
+            if ms is not None:
+                hip.hipEventSynchronize(ev[1])
+                x = C.c_float()
+                hip.hipEventElapsedTime(C.byref(x), ev[0], ev[1])
+                ms.append(x.value)
+
+    for _ in range(args.warmup):
+        step(None)
+    eng.sync()
+    torch.cuda.synchronize()
+    ref = d_dg.cpu().numpy().view(np.uint64).copy()  # (the warm-up pass's digests)
+    d_dg.zero_()
+    replay_ms = []
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step(replay_ms)
+    eng.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    got = d_dg.cpu().numpy().view(np.uint64)
+    dg = np.concatenate([got[k * B:k * B + m] for k, (b0, m) in enumerate(batches)])
+    same = bool(args.warmup == 0 or np.array_equal(got, ref))
+    ok = bool((eng.status() == 0).all()) and same
+    # sampled documents of this rank against the oracle (global ids)
+    threads, affinity, quota = cpu_share()
+    rng = np.random.default_rng(77 + rank)
+    pick = sorted(set(rng.integers(0, n, args.check_docs).tolist()) | {0, n - 1})
+    odg = oracle_digests_random(args, [lo + i for i in pick], threads)
+    ok = ok and bool(np.array_equal(dg[pick], odg))
+    t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, dev)
+    oks = torch.tensor([1.0 if ok else 0.0], device=dev, dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(oks, op=dist.ReduceOp.MIN)
+    ok = bool(oks.item() == 1.0) and int(all_dg.shape[0]) == D
+    nb = len(batches)
+    rms = float(np.mean(replay_ms)) if replay_ms else None  # per k_replay launch (one batch)
+    docs_done = D * args.steps
+    value = docs_done * args.gen_ops / t_max
+    alg_launch = (32 * int(canon.sum()) + 24 * n * args.gen_ops) / nb  # SURVEY 8(d), per launch (batch)
+    achieved = alg_launch / (rms * 1e-3) / 1e9 if rms else None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu:
+            cd, csec = cpu_baseline_random(args, threads, args.cpu_seconds)
+            cpu = {"value": cd * args.gen_ops / csec, "unit": "ops/s", "cores": threads, "threads_used": threads,
+                   "host_cores": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "kind": "port",
+                   "sample": f"{cd} corpus documents x {args.gen_ops} generated ops on the oracle (reference B-tree "
+                             f"restatement, SplitList order index), {threads} threads, one document per task, {csec:.1f} s"}
+        print(json.dumps({
+            "metric": "CRDT ops remapped+merged/sec (whole node)", "value": value, "unit": "ops/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic: make_random_change semantics (doc.rs:544-569) generated in the replay wave",
+            "config": {"workload": f"config4: {D} docs x {args.gen_ops} random-edit ops, document-sharded over "
+                                   f"{world} GPU(s), {nb} resident batch(es) of {B} docs per GPU, replay+publish",
+                       "corpus_docs": D, "ops_per_doc": args.gen_ops, "docs_per_gpu": n, "batch_docs": B,
+                       "batches_per_gpu": nb, "parallelism": f"doc-sharded x{world}",
+                       "waves_per_simd": B / SIMDS, "hbm_bytes_per_batch_doc": mem / B, "hbm_bytes": mem},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                         "traffic": measured_traffic(B, "k_replay", "config4"), "kernel": "k_replay<32>",
+                         "kernel_ms": rms, "alg_bytes_per_launch": alg_launch,
+                         "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops), per batch launch",
+                         "canonical_spans_per_doc": float(canon.sum()) / n},
+            "cpu_baseline": cpu,
+            "parity_ok": ok,
+            "parity": f"all {D} documents' digests equal across the warm-up and timed passes; "
+                      f"{len(pick)} sampled documents per rank == the oracle's replay (global document ids)",
+            "world_size": dist.get_world_size() if dist is not None else 1,
+            "per_rank_ops_s": [n * args.gen_ops * args.steps / t for t in per_rank],
+            "build_id": crdt_amd.build_id(), "stage_s": stage_s,
+        }))
+
+
+# ------------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -404,6 +601,14 @@ def main():
     ap.add_argument("--queries", type=int, default=4096, help="pos->loc and loc->pos queries per document per step")
     ap.add_argument("--rehearse-cpu", action="store_true", help="CPU/gloo rehearsal of the multi-rank plumbing")
     ap.add_argument("--no-stated-size", action="store_true", help="skip the 4,096-document (BASELINE size) leg")
+    ap.add_argument("--workload", choices=["config2", "config4"], default="config2",
+                    help="config2 (default, the driver's line): automerge-paper remote copies; config4: the 1 M-document "
+                         "random-edit corpus")
+    ap.add_argument("--corpus-docs", type=int, default=1_000_000, help="config4: documents in the corpus (all ranks)")
+    ap.add_argument("--batch-docs", type=int, default=125_000, help="config4: documents per resident batch")
+    ap.add_argument("--gen-ops", type=int, default=20_000, help="config4: generated ops per document")
+    ap.add_argument("--seed", type=int, default=0xC0FFEE, help="config4: corpus seed")
+    ap.add_argument("--check-docs", type=int, default=64, help="config4: sampled documents per rank checked against the oracle")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the multi-rank path on one GPU: every rank runs its engine on cuda:0 and "
                          "the collectives go over gloo (CPU tensors); not a scaling measurement")
@@ -423,7 +628,10 @@ def main():
         if world > 1:
             import torch.distributed as dist
             dist.init_process_group("gloo")
-        rehearse_cpu(args, world, rank, dist)
+        if args.workload == "config4":
+            run_config4(args, world, rank, 0, dist)
+        else:
+            rehearse_cpu(args, world, rank, dist)
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -436,6 +644,11 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         dist.init_process_group("gloo" if args.share_gpu else "nccl")
+    if args.workload == "config4":
+        run_config4(args, world, rank, gpu, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     import crdt_amd
     from crdt_amd.traces import load_remote_wire
 

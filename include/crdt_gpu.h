@@ -202,6 +202,20 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
 // crdt_run + publish of it; a later reset + crdt_run_async replays it in exactly that room).
 // Capacities grow again on the next stage.  (Host-side planning; no reference counterpart.)
 int crdt_fit(crdt_engine* e);
+// crdt_fit over several corpora replayed one after another on the same documents (BASELINE config
+// 4's batches): apply = 0 notes the capacities crdt_fit would set into each document's running
+// maximum (no relayout); apply = 1 sets every document's capacities to its noted maximum (one
+// relayout) and forgets the maxima.  (Host-side planning; no reference counterpart.)
+int crdt_fit_note(crdt_engine* e, int apply);
+// Config 4 corpus batches: every document whose staged stream is one generated-edit record
+// (crdt_stage_random) gets the seed crdt_stage_random would give document id_base + d
+// ((u32)splitmix64(seed ^ (id_base + d)); the generator follows make_random_change,
+// /root/reference/src/list/doc.rs:544-569).  Device-side, async on the engine stream; the next
+// reset + crdt_run_async replays the new documents.
+int crdt_reseed_random_async(crdt_engine* e, uint64_t seed, uint64_t id_base);
+// crdt_digest into a device buffer (n_docs u64), async on the engine stream after the publish
+// that computes the digests (crdt_publish_async).
+int crdt_digest_dev_async(crdt_engine* e, uint64_t* dev_out);
 // on != 0: documents staged in one call from the same host stream (crdt_stage_local_shared,
 // crdt_stage_remote_replicated) read one device copy of it instead of a copy each (records
 // are read-only input).  Off by default.
@@ -225,6 +239,10 @@ uint64_t crdt_mem_bytes(const crdt_engine* e);
 // they held at once since the last reset (a relayout -- growth, crdt_fit -- moves the pools one
 // at a time: its peak is the old pools + the largest new one).  Diagnostic; never fails.
 int crdt_device_bytes(uint64_t* current, uint64_t* peak, int reset_peak);
+// Test hook: after k more device allocations by any engine of this process, the next one fails as
+// out of memory (k < 0: never).  A relayout that fails part-way poisons its engine: every later
+// call but crdt_engine_destroy / crdt_docs_alloc returns CRDT_E_NOMEM.
+int crdt_test_fail_alloc_after(long long k);
 // Config 1's per-op check: after txn t (of every listed document), ask pos_to_loc(probes[t].pos)
 // and loc_to_pos(probes[t].agent, probes[t].seq) on the state reached so far (the README's two
 // mappings, cursor.rs:147-190 count_pos; answers as crdt_pos_to_loc / crdt_loc_to_pos).

@@ -32,7 +32,7 @@ a = ap.parse_args()
 
 import crdt_amd  # noqa: E402
 from crdt_amd.traces import load_trace  # noqa: E402
-from bench import splitmix64, cpu_share, cpu_baseline_local, sampled, SIMDS  # noqa: E402
+from bench import splitmix64, cpu_share, cpu_baseline_local, sampled, measured_traffic, SIMDS, HBM_PEAK_GBS  # noqa: E402
 
 names = ["automerge-paper", "rustcode", "sveltecomponent"]
 traces = [load_trace(n) for n in names]
@@ -77,6 +77,10 @@ dg = e.digests()
 want = np.array([int(gold[f"{names[k]}/L32"]["digest"], 16) for k in which], np.uint64)
 ok = bool((e.status() == 0).all()) and bool((dg == want).all())
 ops = int(sum(traces[k].n_patches for k in which))
+canon_total = int(e.canon_counts().astype(np.int64).sum())
+rk = float(np.mean(rms))
+alg = 32 * canon_total + 24 * ops  # docs x (32 B x canonical spans + 24 B x ops)
+wl = "config3" if a.share else "config3_noshare"
 # CPU leg: the oracle replaying the same mix on every core this process may use
 threads, affinity, quota = cpu_share()
 mix = np.bincount(which, minlength=3) / a.docs
@@ -94,7 +98,12 @@ print(json.dumps({
                "ops": ops, "mix": {n: int((which == k).sum()) for k, n in enumerate(names)},
                "record_streams": "one device copy per trace (read-only input)" if a.share else "one copy per document",
                "waves_per_simd": a.docs / SIMDS, "hbm_bytes_per_doc": mem / a.docs, "hbm_bytes": mem},
-    "kernels_ms": {"k_replay": float(np.mean(rms)), "k_publish": float(np.mean(pms))},
+    "roofline": {"bound": "hbm", "achieved": alg / (rk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": alg / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": measured_traffic(a.docs, "k_replay", wl),
+                 "traffic_file": f"profiles/traffic_k_replay_{wl}.json", "kernel": "k_replay<32>", "kernel_ms": rk,
+                 "alg_bytes_per_launch": alg, "canonical_spans": canon_total,
+                 "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops)"},
+    "kernels_ms": {"k_replay": rk, "k_publish": float(np.mean(pms))},
     "cpu_baseline": {"value": cpu_ops / cpu_s, "unit": "ops/s", "threads_used": threads, "host_cores": os.cpu_count(),
                      "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "kind": "port",
                      "sample": f"oracle (reference B-tree restatement, SplitList index) on the same mix, {cpu_s:.1f} s"},

@@ -2,6 +2,10 @@
 // using the same host planning code as the engine, and exports the resulting state in the
 // oracle's export format so tests can diff the GPU algorithm against the oracle without a GPU.
 #define CRDT_EMU_CHECKS 1  // replay preconditions checked (crdt_types.h CRDT_EXPECT)
+#ifdef CRDT_EMU_STATS  // statistics build (make stats): event counters of replay_core.h's CRDT_STAT sites
+static unsigned long long g_stat[128];
+#define CRDT_STAT(k, v) (g_stat[(k)] += (unsigned long long)(v))
+#endif
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -187,6 +191,11 @@ void* emu_new(uint32_t leaf_cap) {
   return d;
 }
 void emu_free(void* h) { delete (EmuDoc*)h; }
+#ifdef CRDT_EMU_STATS
+void emu_stats(uint64_t* out, int reset) {
+  for (int k = 0; k < 128; k++) { out[k] = g_stat[k]; if (reset) g_stat[k] = 0; }
+}
+#endif
 int emu_agent(void* h, const char* name) { return (int)((EmuDoc*)h)->agents.get_or_create(name); }
 
 // Apply a local trace (as one stream) to a fresh emulated document.

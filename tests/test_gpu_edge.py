@@ -261,3 +261,98 @@ def test_rejected_stage_leaves_agent_ids_unchanged():
     assert o.apply_remote_wire(w2) == 0
     assert_same(e.export(1), o.export())
     assert int(e.digests()[1]) == o.digest()
+
+
+def test_failed_relayout_poisons_the_engine():
+    # a growth relayout that runs out of device memory after it began moving pools must
+    # not leave a half-moved engine usable.  The k-th device allocation of a staging call that grows
+    # every document is made to fail, for every k until the call no longer fails: either nothing
+    # had moved yet (the engine keeps its state: same digests) or the engine is poisoned (every
+    # later call but destroy / docs_alloc answers CRDT_E_NOMEM, and a fresh docs_alloc works).
+    from crdt_amd.traces import load_trace
+    t = load_trace("sveltecomponent")
+    o = OracleDoc()
+    o.apply_trace(o.agent("jeremy"), t.counts, t.patches)
+    L = crdt_amd.lib()
+    h50 = int(t.counts[:50].sum())
+    poisoned = intact = 0
+    for k in range(64):
+        e = crdt_amd.Engine(2, 32)
+        ag = int(e.agent_intern([0, 1], ["jeremy"] * 2)[0])
+        assert (e.apply_trace([0, 1], ag, t.counts[:50], t.patches[:h50]) == 0).all()
+        d1 = e.digests()
+        L.crdt_test_fail_alloc_after(k)
+        try:
+            e.apply_trace([0, 1], ag, t.counts[50:], t.patches[h50:], stage_only=True)
+            failed = False
+        except crdt_amd.CrdtError:
+            failed = True
+        finally:
+            L.crdt_test_fail_alloc_after(-1)
+        if not failed:
+            e.close()
+            break
+        try:
+            d = e.digests()
+        except crdt_amd.CrdtError as x:
+            assert "rc=-102" in str(x), x
+            poisoned += 1
+            with pytest.raises(crdt_amd.CrdtError, match="rc=-102"):
+                e.run()
+            with pytest.raises(crdt_amd.CrdtError, match="rc=-102"):
+                e.pos_to_loc(np.zeros(1, np.uint32), np.zeros(1, np.uint32))
+            # a fresh allocation of the documents makes the engine usable again
+            assert L.crdt_docs_alloc(e.h, 1) == 0
+            e.n_docs = 1
+            ag = int(e.agent_intern([0], ["jeremy"])[0])
+            assert e.apply_trace([0], ag, t.counts, t.patches)[0] == 0
+            assert int(e.digests()[0]) == o.digest()
+        else:
+            intact += 1
+            assert (d == d1).all(), k  # (failed before anything moved)
+        e.close()
+    else:
+        raise AssertionError("every allocation of the staging call failed")
+    assert poisoned >= 5, (poisoned, intact)  # (the relayout moves ~20 pools one at a time)
+
+
+def test_config4_batches_reseed_and_fit_note():
+    # bench.py --workload config4: one engine replays the batches of a larger corpus.  Documents
+    # reseeded to corpus ids id_base + d replay exactly what stage_random gives those ids, the
+    # capacities noted over every batch (fit_note) hold each batch without growth, and the
+    # device digest copy equals crdt_digest.
+    import torch
+    n, ops, seed = 24, 3000, 0xC0FFEE
+    big = crdt_amd.Engine(3 * n, 32)
+    big.stage_random(list(range(3 * n)), "gen", ops, seed)
+    assert (big.run() == 0).all()
+    want = big.digests()
+    e = crdt_amd.Engine(n, 32)
+    e.stage_random(list(range(n)), "gen", ops, seed)
+    for b in range(3):
+        e.reseed_random_async(seed, b * n)
+        e.reset_async()
+        assert (e.run() == 0).all()
+        e.publish_async()
+        e.sync()
+        assert (e.digests() == want[b * n:(b + 1) * n]).all(), b
+        e.fit_note(False)
+    e.fit_note(True)
+    d = torch.zeros(n, dtype=torch.int64, device="cuda")
+    for b in (2, 0, 1):
+        e.reseed_random_async(seed, b * n)
+        e.reset_async()
+        e.run_async()
+        e.publish_async()
+        e.digests_dev_async(d.data_ptr())
+        e.sync()
+        assert (e.status() == 0).all()  # (no capacity stop: the noted maximum holds every batch)
+        assert (d.cpu().numpy().view(np.uint64) == want[b * n:(b + 1) * n]).all(), b
+    # the oracle agrees with a sampled corpus document (global id 2n + 5)
+    o = OracleDoc(32, 16)
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import splitmix64
+    assert o.apply_random(o.agent("gen"), ops, splitmix64(seed ^ (2 * n + 5)) & 0xFFFFFFFF) == 0
+    assert int(want[2 * n + 5]) == o.digest()

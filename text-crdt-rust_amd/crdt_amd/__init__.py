@@ -192,6 +192,11 @@ def lib():
     L.crdt_stage_local_shared.argtypes = [vp, u64, P(u32), P(u32), u32, P(u64), vp, vp]
     L.crdt_debug_state.argtypes = [vp, u32, P(u32)]
     L.crdt_fit.argtypes = [vp]
+    # (round-5 entry points; a diagnostic library from before them (CRDT_GPU_LIB) loads without them)
+    for f, at in (("crdt_fit_note", [vp, C.c_int]), ("crdt_test_fail_alloc_after", [C.c_longlong]),
+                  ("crdt_reseed_random_async", [vp, u64, u64]), ("crdt_digest_dev_async", [vp, vp])):
+        if hasattr(L, f):
+            getattr(L, f).argtypes = at
     L.crdt_set_share_streams.argtypes = [vp, C.c_int]
     for f in ("crdt_set_device_intern", "crdt_set_query_kernel"):
         if hasattr(L, f):  # (older libraries, for A/B runs, lack them)
@@ -246,6 +251,7 @@ EXPORTED_SYMBOLS = [
     "crdt_stream", "crdt_last_error", "crdt_build_id", "crdt_stage_random", "crdt_debug_state",
     "crdt_stage_local_shared", "crdt_set_content", "crdt_materialize_async", "crdt_text", "crdt_text_digest",
     "crdt_last_materialize_ms", "crdt_set_content_copies", "crdt_canon_counts", "crdt_fit", "crdt_mem_bytes", "crdt_apply_local_probed", "crdt_set_share_streams", "crdt_set_device_intern", "crdt_set_query_kernel", "crdt_device_bytes",
+    "crdt_fit_note", "crdt_reseed_random_async", "crdt_digest_dev_async", "crdt_test_fail_alloc_after",
     # include/crdt_trace.h (host-only trace ingestion)
     "crdt_trace_load", "crdt_trace_parse", "crdt_trace_sizes", "crdt_trace_copy", "crdt_trace_free",
 ]
@@ -420,6 +426,20 @@ class Engine:
     def fit(self):
         """shrink capacities to the staged streams' use (after run + publish)"""
         _check(self.L.crdt_fit(self.h), "fit")
+
+    def fit_note(self, apply: bool = False):
+        """apply=False: note the capacities fit() would set into each document's running maximum;
+        apply=True: capacities = the noted maxima (config 4 corpus batches on one engine)"""
+        _check(self.L.crdt_fit_note(self.h, int(apply)), "fit_note")
+
+    def reseed_random_async(self, seed: int, id_base: int):
+        """generated-edit documents (stage_random) become documents id_base + d of the corpus"""
+        _check(self.L.crdt_reseed_random_async(self.h, C.c_uint64(seed & 0xFFFFFFFFFFFFFFFF), C.c_uint64(id_base)),
+               "reseed_random_async")
+
+    def digests_dev_async(self, dev_ptr: int):
+        """copy the per-document digests to a device buffer (n_docs u64) on the engine stream"""
+        _check(self.L.crdt_digest_dev_async(self.h, C.c_void_p(dev_ptr)), "digest_dev_async")
 
     def share_streams(self, on: bool = True):
         """documents staged from the same host stream read one device copy"""

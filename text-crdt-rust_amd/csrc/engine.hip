@@ -36,10 +36,16 @@ thread_local std::string g_last_error;
 std::mutex g_mem_mu;
 std::unordered_map<void*, u64> g_mem_size;
 u64 g_mem_cur = 0, g_mem_peak = 0;
+long long g_fail_alloc_after = -1;  // crdt_test_fail_alloc_after: the allocations left before one fails
 template <class T>
 hipError_t dalloc(T*& p, u64 n) {
   p = nullptr;
   if (n == 0) n = 1;
+  {
+    std::lock_guard<std::mutex> g(g_mem_mu);
+    if (g_fail_alloc_after == 0) return hipErrorOutOfMemory;
+    if (g_fail_alloc_after > 0) g_fail_alloc_after--;
+  }
   hipError_t e = hipMalloc((void**)&p, sizeof(T) * n);
   if (e == hipSuccess) {
     std::lock_guard<std::mutex> g(g_mem_mu);
@@ -94,10 +100,20 @@ struct DocHost {
   StreamNeeds cum;          // needs of every stream applied since the last reset (capacity plan)
   StreamNeeds staged;       // needs of the stream staged now (a reset replays it: cum = staged)
   Caps caps{};              // current capacities (grow; crdt_fit shrinks them to the replay's use)
+  Caps fit_max{};           // crdt_fit_note: per-field maximum of the fitted capacities noted so far
+  bool fit_noted = false;
   bool tracked = false;     // keeps the order -> leaf map (once a remote stream was staged)
   bool agent_map = false;   // keeps the order -> agent map (tracked, and more than one agent)
   std::vector<u32> agent_cap;
 };
+
+// field-wise maximum of two capacity plans (crdt_fit_note)
+inline void caps_max(Caps& a, const Caps& b) {
+  static_assert(sizeof(Caps) % 4 == 0, "Caps is u32 fields");
+  u32* x = (u32*)&a;
+  const u32* y = (const u32*)&b;
+  for (size_t k = 0; k < sizeof(Caps) / 4; k++) x[k] = std::max(x[k], y[k]);
+}
 
 inline void add_needs(StreamNeeds& c, const StreamNeeds& n) {
   c.n_txn += n.n_txn; c.n_ltxn += n.n_ltxn; c.n_rtxn += n.n_rtxn; c.n_ops += n.n_ops; c.orders += n.orders;
@@ -193,6 +209,10 @@ struct crdt_engine {
   bool intern_on_device = false;  // crdt_stage_remote_replicated interns through k_intern
   int query_kernel = -1;  // crdt_set_query_kernel (-1: not set; CRDT_QUERY_PER_THREAD selects 1)
   bool published = false;
+  // A relayout (growth, crdt_fit) that failed after it began moving pools leaves some pools at
+  // their new bases and the rest at the old ones: the engine is then unusable, and every call but
+  // release / crdt_docs_alloc returns CRDT_E_NOMEM (no half-moved engine is replayed).
+  bool poisoned = false;
   int qmode() const {
     if (query_kernel >= 0) return query_kernel;
     static const bool per_thread = getenv("CRDT_QUERY_PER_THREAD") != nullptr;  // (A/B switch)
@@ -304,6 +324,7 @@ struct crdt_engine {
     if (r) return r;
     HIPCHK(hipStreamSynchronize(stream));
     release();
+    poisoned = false;
     n_docs = n;
     docs.assign(n, DocHost{});
     seg_h.assign(n, DocSeg{});
@@ -385,9 +406,11 @@ struct crdt_engine {
       nseg[d] = s;
     }
     // sizes of the new pools (element counts; 0 -> one element)
-    const u64 n_lag = nl * lag_words(L);
+    // leaf agent rows only when some document keeps the order -> agent map: the others never read
+    // or store a row (lag_stale is a lane-predicated store on K_AGMAP), so the pool is one element
+    const u64 n_lag = any_agent_map ? nl * lag_words(L) : 1;
     const u64 n_agent_of = any_agent_map ? nm : 1, n_hrows = any_hroot ? nhr * HROOT_ROW : 1, n_gsob = any_hroot ? nb : 1;
-    np.bytes = nl * L * 16 + nl * 8 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) + nl * lag_words(L) * 4 +
+    np.bytes = nl * L * 16 + nl * 8 + nb * GROUP * 8 + nm * 4 + (any_agent_map ? nm * 2 : 0) + n_lag * 4 +
                (any_hroot ? nhr * HROOT_ROW * 4 + nb * 4 : 0) + nc * 16 + na * 16 + ndl * 12 +
                ndd * (DD_BLK * 12 + 16) + nt * 32 + npar * 4 + nag * (u64)sizeof(AgentRec) + nfr * 4 + nb * 16;
     if (getenv("CRDT_DEBUG_MEM"))
@@ -395,11 +418,19 @@ struct crdt_engine {
               (unsigned long long)nl, (unsigned long long)nb, (unsigned long long)nm, (unsigned long long)nc,
               (unsigned long long)na, (unsigned long long)ndl, (unsigned long long)ndd, (unsigned long long)nt,
               (unsigned long long)npar, (unsigned long long)nag, (unsigned long long)nfr, np.bytes / 1e6);
+    // From here on the engine's state changes pool by pool: until the last pool has moved, a
+    // failure leaves it poisoned (and frees what this call allocated).
+    poisoned = true;
+    DocSeg* old_segs = nullptr;
+    struct Cleanup {
+      PoolSet& np;
+      DocSeg*& os;
+      ~Cleanup() { dfree(np.agents); dfree(os); }
+    } cleanup{np, old_segs};
     HIPCHK(dalloc(np.agents, nag));  // (the new agent table first: the run move reads its bases)
     if (!agent_tab.empty())
       HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(n_agents_d, n_agents.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
-    DocSeg* old_segs = nullptr;
     if (move) {
       HIPCHK(dalloc(old_segs, n_docs));
       HIPCHK(hipMemcpyAsync(old_segs, segs, n_docs * sizeof(DocSeg), hipMemcpyDeviceToDevice, stream));
@@ -442,7 +473,7 @@ struct crdt_engine {
     if (!r) r = step(pools.frontier, np.frontier, nfr, RL_FRONTIER);
     if (!r) r = step(pools.groups, np.groups, nb, RL_GROUPS);
     if (!r) r = step(pools.arun, np.arun, na, RL_ARUN);
-    if (r) { dfree(old_segs); return r; }
+    if (r) return r;
     if (move) {  // the agents' run counts and last-run copies into the new table
       Pools src = pools_view(pools), dst = pools_view(pools);
       dst.agents = np.agents;
@@ -451,12 +482,12 @@ struct crdt_engine {
       HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(stream));
-    dfree(old_segs);
     dfree(pools.agents);
     pools.agents = np.agents;
     np.agents = nullptr;
     pools.bytes = np.bytes;
     seg_h = nseg;
+    poisoned = false;
     r = plan_classes();
     if (r) return r;
     pub_sized = false;
@@ -689,16 +720,21 @@ struct crdt_engine {
       for (auto* s : streams)
         if (!share || seen.emplace(s, 1).second) total += s->size();
     }
-    if (total > rec_cap) {
+    if (total > rec_cap) {  // (the new buffer first: a failed allocation leaves the old one in place)
+      Rec* nr = nullptr;
+      u64 cap = std::max<u64>(total, 1024);
+      HIPCHK(dalloc(nr, cap));
       dfree(recs);
-      rec_cap = std::max<u64>(total, 1024);
-      HIPCHK(dalloc(recs, rec_cap));
+      recs = nr;
+      rec_cap = cap;
     }
     has_probes = n_probes > 0;
     if (has_probes && probe_cap < total) {
+      uint4* np_ = nullptr;
+      HIPCHK(dalloc(np_, total));
       dfree(probe);
+      probe = np_;
       probe_cap = total;
-      HIPCHK(dalloc(probe, probe_cap));
     }
     if (has_probes) {
       // every probe slot starts as the "unknown" answer: probes after a document's stop point
@@ -875,7 +911,9 @@ struct crdt_engine {
   // Shrink every document's capacities to what its staged stream used, keeping the room the
   // replay reserves ahead of one txn (fits()): called after a full replay + publish of the staged
   // streams, so that replaying them again (reset + run) needs exactly this much.
-  int fit() {
+  // mode 0: fit (capacities = what the staged streams used); 1: note those capacities into each
+  // document's running maximum (no relayout); 2: capacities = the noted maxima (and forget them)
+  int fit(int mode = 0) {
     int r = ensure_published();
     if (r) return r;
     r = pull_states();
@@ -887,7 +925,8 @@ struct crdt_engine {
       if (s.status != ST_OK) continue;
       DocHost& h = docs[d];
       const StreamNeeds& m = h.cum;
-      Caps& c = h.caps;
+      Caps fc = h.caps;
+      Caps& c = mode == 0 ? h.caps : fc;
       c.leaf = std::max<u32>(s.n_leaves + 2 * m.max_ops + 2, 2);
       c.blk = blk_cap_for(c.leaf);
       c.cwo = s.n_cwo + 1;
@@ -904,7 +943,15 @@ struct crdt_engine {
         u64 ov = std::min<u64>(s.n_dd, m.max_rdel_len);
         c.dd = std::max<u32>(4u, (u32)std::min<u64>(((u64)s.n_dd + 3 * ov + 2ull * m.max_rdel_len + 2) / 32 + 3, 0x7FFFFFFFull));
       }
+      if (mode == 0) continue;
+      if (!h.fit_noted) { h.fit_max = fc; h.fit_noted = true; }
+      else caps_max(h.fit_max, fc);
+      if (mode == 2) {
+        h.caps = h.fit_max;
+        h.fit_noted = false;
+      }
     }
+    if (mode == 1) return 0;
     r = layout(true);
     if (r) return r;
     r = size_pub();
@@ -1083,6 +1130,11 @@ struct crdt_engine {
 };
 
 static bool valid(const crdt_engine* e) { return e && e->n_docs > 0; }
+static bool poisoned(const crdt_engine* e) {
+  if (!e || !e->poisoned) return false;
+  g_last_error = "engine poisoned: a relayout failed part-way (out of device memory); destroy it or crdt_docs_alloc again";
+  return true;
+}
 // The documents a stage call names: in range and none twice (checked before any interning, so a
 // rejected call leaves every agent table -- and so the agent ids of later calls -- unchanged)
 static bool ids_ok(const crdt_engine* e, uint64_t n, const uint32_t* docs) {
@@ -1143,7 +1195,14 @@ int crdt_docs_alloc(crdt_engine* e, uint64_t n) {
 }
 uint64_t crdt_num_docs(const crdt_engine* e) { return e ? e->n_docs : 0; }
 
+int crdt_test_fail_alloc_after(long long k) {
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  g_fail_alloc_after = k < 0 ? -1 : k;
+  return 0;
+}
+
 int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const char* const* names, uint16_t* out) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || (n && (!doc || !names || !out))) return CRDT_E_ARG;
   for (uint64_t i = 0; i < n; i++) {
     if (doc[i] >= e->n_docs) return CRDT_E_ARG;
@@ -1157,6 +1216,7 @@ int crdt_agent_intern(crdt_engine* e, uint64_t n, const uint32_t* doc, const cha
 // first-appearance numbering reproduces their ids) followed by this call's names for it.
 int crdt_agent_intern_dev(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint64_t* name_off,
                           const char* bytes, uint16_t* out, uint32_t* rank_out) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || (n && (!doc || !name_off || !bytes || !out))) return CRDT_E_ARG;
   if (!n) return 0;
   int rs = e->set_device();  // (scratch and the launch belong on the engine's device)
@@ -1270,6 +1330,7 @@ int crdt_agent_intern_dev(crdt_engine* e, uint64_t n, const uint32_t* doc, const
 static int stage_local_impl(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint64_t* txn_off,
                             const crdt_local_txn* txns, const crdt_local_op* ops,
                             const crdt_probe* probes = nullptr, std::vector<std::vector<u32>>* probe_rec = nullptr) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !docs || !txn_off || (!txns && txn_off[n_docs]) ) return CRDT_E_ARG;
   if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   if (probe_rec) probe_rec->assign(n_docs, {});
@@ -1327,6 +1388,7 @@ int crdt_stage_local(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, cons
 int crdt_stage_local_shared(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* stream_of_doc,
                             uint32_t n_streams, const uint64_t* stream_txn_off, const crdt_local_txn* txns,
                             const crdt_local_op* ops) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !docs || !stream_of_doc || !stream_txn_off || !n_streams) return CRDT_E_ARG;
   if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   std::vector<std::vector<Rec>> enc(n_streams);
@@ -1352,6 +1414,7 @@ int crdt_stage_local_shared(crdt_engine* e, uint64_t n_docs, const uint32_t* doc
 
 int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint8_t* const* wire,
                            const uint64_t* wire_len) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !docs || !wire || !wire_len) return CRDT_E_ARG;
   if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   std::vector<u64> ids(n_docs);
@@ -1371,6 +1434,7 @@ int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs
 
 int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t wire_len, uint32_t rename_idx,
                                  const char* const* names) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !wire) return CRDT_E_ARG;
   WireView wv;
   if (!wv.parse(wire, wire_len)) return CRDT_E_WIRE;
@@ -1452,6 +1516,7 @@ int crdt_stage_remote_replicated(crdt_engine* e, const uint8_t* wire, uint64_t w
 
 int crdt_stage_random(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const char* agent, uint32_t n_ops,
                       uint64_t seed) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !docs || !agent || n_ops == 0 || std::strcmp(agent, "ROOT") == 0) return CRDT_E_ARG;
   if (!ids_ok(e, n_docs, docs)) return CRDT_E_ARG;
   std::vector<u64> ids(n_docs);
@@ -1469,6 +1534,7 @@ int crdt_stage_random(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, con
 }
 
 int crdt_reset_async(crdt_engine* e) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
@@ -1479,11 +1545,13 @@ int crdt_reset_async(crdt_engine* e) {
 }
 
 int crdt_run(crdt_engine* e, int32_t* doc_status) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   return e->run(doc_status);
 }
 
 int crdt_run_async(crdt_engine* e) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
@@ -1491,6 +1559,7 @@ int crdt_run_async(crdt_engine* e) {
 }
 
 int crdt_publish_async(crdt_engine* e) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   return e->publish();
 }
@@ -1544,13 +1613,46 @@ int crdt_set_device_intern(crdt_engine* e, int on) {
 }
 
 int crdt_fit(crdt_engine* e) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
   return e->fit();
 }
 
+int crdt_fit_note(crdt_engine* e, int apply) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
+  if (!valid(e)) return CRDT_E_ARG;
+  int r = e->set_device();
+  if (r) return r;
+  return e->fit(apply ? 2 : 1);
+}
+
+int crdt_reseed_random_async(crdt_engine* e, uint64_t seed, uint64_t id_base) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
+  if (!valid(e)) return CRDT_E_ARG;
+  int r = e->set_device();
+  if (r) return r;
+  if (!e->n_docs) return 0;
+  hipLaunchKernelGGL(k_reseed_gen, dim3((u32)((e->n_docs + 255) / 256)), dim3(256), 0, e->stream, e->pools_view(e->pools),
+                     (u32)e->n_docs, (u64)seed, (u64)id_base);
+  HIPCHK(hipGetLastError());
+  e->published = false;
+  e->materialized = false;
+  return 0;
+}
+
+int crdt_digest_dev_async(crdt_engine* e, uint64_t* dev_out) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
+  if (!valid(e) || !dev_out) return CRDT_E_ARG;
+  int r = e->set_device();
+  if (r) return r;
+  HIPCHK(hipMemcpyAsync(dev_out, e->digest, e->n_docs * 8, hipMemcpyDeviceToDevice, e->stream));
+  return 0;
+}
+
 int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint32_t* pos, uint16_t* agent, uint32_t* seq) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   if (!e->published) {
     int r = e->publish();
@@ -1578,6 +1680,7 @@ int crdt_pos_to_loc_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
 }
 
 int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint16_t* agent, const uint32_t* seq, uint32_t* pos, uint8_t* deleted) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   if (!e->published) {
     int r = e->publish();
@@ -1602,6 +1705,7 @@ int crdt_loc_to_pos_dev_async(crdt_engine* e, uint64_t n, const uint32_t* doc, c
 }
 
 int crdt_pos_to_loc(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint32_t* pos, uint16_t* agent, uint32_t* seq) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || (n && (!doc || !pos || !agent || !seq))) return CRDT_E_ARG;
   if (!n) return 0;
   int r = e->ensure_published();
@@ -1625,6 +1729,7 @@ int crdt_pos_to_loc(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint3
 }
 
 int crdt_loc_to_pos(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint16_t* agent, const uint32_t* seq, uint32_t* pos, uint8_t* deleted) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || (n && (!doc || !agent || !seq || !pos || !deleted))) return CRDT_E_ARG;
   if (!n) return 0;
   int r = e->ensure_published();
@@ -1650,6 +1755,7 @@ int crdt_loc_to_pos(crdt_engine* e, uint64_t n, const uint32_t* doc, const uint1
 }
 
 int crdt_doc_len(crdt_engine* e, uint64_t n, const uint32_t* doc, uint32_t* len) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || (n && (!doc || !len))) return CRDT_E_ARG;
   int r = e->pull_states();
   if (r) return r;
@@ -1661,6 +1767,7 @@ int crdt_doc_len(crdt_engine* e, uint64_t n, const uint32_t* doc, uint32_t* len)
 }
 
 int crdt_doc_status(crdt_engine* e, int32_t* status) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !status) return CRDT_E_ARG;
   int r = e->pull_states();
   if (r) return r;
@@ -1669,6 +1776,7 @@ int crdt_doc_status(crdt_engine* e, int32_t* status) {
 }
 
 int crdt_digest(crdt_engine* e, uint64_t* per_doc) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !per_doc) return CRDT_E_ARG;
   int r = e->ensure_published();
   if (r) return r;
@@ -1678,6 +1786,7 @@ int crdt_digest(crdt_engine* e, uint64_t* per_doc) {
 }
 
 int crdt_canon_counts(crdt_engine* e, uint32_t* per_doc) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !per_doc) return CRDT_E_ARG;
   int r = e->ensure_published();
   if (r) return r;
@@ -1688,6 +1797,7 @@ int crdt_canon_counts(crdt_engine* e, uint32_t* per_doc) {
 
 // Export: walk the document's directory on the host from device copies.
 int crdt_export_sizes(crdt_engine* e, uint32_t doc, uint64_t* s) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || doc >= e->n_docs || !s) return CRDT_E_ARG;
   int r = e->ensure_published();
   if (r) return r;
@@ -1758,6 +1868,7 @@ int crdt_export(crdt_engine* e, uint32_t doc, uint32_t* raw4, uint32_t* leaf_siz
 }
 
 int crdt_debug_state(crdt_engine* e, uint32_t doc, uint32_t* out23) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || doc >= e->n_docs || !out23) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
@@ -1792,6 +1903,7 @@ void* crdt_stream(crdt_engine* e) { return e ? (void*)e->stream : nullptr; }
 
 int crdt_set_content(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* stream_of_doc,
                      uint32_t n_streams, const uint64_t* stream_off, const uint32_t* content) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || (n_docs && (!docs || !stream_of_doc)) || !stream_off || (stream_off[n_streams] && !content))
     return CRDT_E_ARG;
   return e->set_content(n_docs, docs, stream_of_doc, n_streams, stream_off, content);
@@ -1799,16 +1911,19 @@ int crdt_set_content(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, cons
 
 int crdt_set_content_copies(crdt_engine* e, uint64_t n_docs, const uint32_t* docs, const uint32_t* content,
                             uint64_t len) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || (n_docs && !docs) || (len && !content)) return CRDT_E_ARG;
   return e->set_content_copies(n_docs, docs, content, len);
 }
 
 int crdt_materialize_async(crdt_engine* e) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e)) return CRDT_E_ARG;
   return e->materialize();
 }
 
 int crdt_text(crdt_engine* e, uint32_t doc, uint32_t* out, uint64_t cap, uint64_t* n_out) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || doc >= e->n_docs || !n_out) return CRDT_E_ARG;
   int r = e->ensure_materialized();
   if (r) return r;
@@ -1823,6 +1938,7 @@ int crdt_text(crdt_engine* e, uint32_t doc, uint32_t* out, uint64_t cap, uint64_
 }
 
 int crdt_text_digest(crdt_engine* e, uint64_t* per_doc) {
+  if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !per_doc) return CRDT_E_ARG;
   int r = e->ensure_materialized();
   if (r) return r;

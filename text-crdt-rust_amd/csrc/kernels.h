@@ -117,6 +117,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   replay_doc<L, true>(P, n, wpb, rcap, list);
 }
 
+// crdt_reseed_random_async: every document whose staged stream is one GEN record (crdt_stage_random)
+// gets the generator seed of document id_base + d, (u32)mix64(seed ^ (id_base + d)) -- the seed
+// crdt_stage_random gives document d for id_base 0 -- so one engine replays the batches of a
+// larger corpus (BASELINE config 4: 1 M documents) without restaging.  Other documents are untouched.
+__global__ void k_reseed_gen(Pools P, u32 n, u64 seed, u64 id_base) {
+  u32 d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  DocSeg sg = P.seg[d];
+  if (sg.rec_n != 1u) return;
+  Rec* r = const_cast<Rec*>(P.recs + sg.rec_base);  // (the staged record pool: read-only to the replay)
+  if (rec_kind(*r) != REC_GEN) return;
+  r->w3 = (u32)mix64(seed ^ (id_base + d));
+}
+
 // Reset the per-call record cursor of every document (new stream staged).
 __global__ void k_reset_recpos(DocState* st, u32 n, u32 n_agents_dummy) {
   u32 d = blockIdx.x * blockDim.x + threadIdx.x;
@@ -696,7 +710,7 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
 // ---------------------------------------------------------------------------------------------
 #define PUBX_THREADS 256
 #define PUBX_MAX_WORDS 16384u  // bitmaps up to 524,288 orders (72 KiB of LDS: two blocks per CU)
-CRDT_HD inline u32 pubx_lds_bytes(u32 xw) { return (xw + xw / 8u + 1u) * 4u; }
+CRDT_HD u32 pubx_lds_bytes(u32 xw) { return (xw + xw / 8u + 1u) * 4u; }
 
 __global__ __launch_bounds__(PUBX_THREADS) void k_pub_index(Pools P, PubOut O, const u32* list, u32 xw) {
   extern __shared__ u32 xl[];
