@@ -29,7 +29,7 @@ ap.add_argument("--cpu-seconds", type=float, default=15.0)
 a = ap.parse_args()
 
 import crdt_amd  # noqa: E402
-from bench import splitmix64, cpu_share, SIMDS, HBM_PEAK_GBS  # noqa: E402
+from bench import splitmix64, cpu_share, measured_traffic, SIMDS, HBM_PEAK_GBS  # noqa: E402
 
 e = crdt_amd.Engine(a.docs, 32)
 t0 = time.time()
@@ -106,7 +106,8 @@ print(json.dumps({
                "docs_per_gpu": a.docs, "ops_per_doc": a.ops, "waves_per_simd": a.docs / SIMDS,
                "hbm_bytes_per_doc": mem / a.docs, "hbm_bytes": mem},
     "roofline": {"bound": "hbm", "achieved": alg / (rk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": alg / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": "k_replay<32>",
+                 "frac": alg / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": measured_traffic(a.docs, "k_replay", "config4"),
+                 "kernel": "k_replay<32>",
                  "kernel_ms": rk, "alg_bytes_per_launch": alg, "canonical_spans": canon_total,
                  "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops)"},
     "kernels_ms": {"k_replay": rk, "k_publish": float(np.mean(pms))},

@@ -39,7 +39,7 @@ ap.add_argument("--no-cpu", action="store_true")
 a = ap.parse_args()
 
 import crdt_amd  # noqa: E402
-from bench import cpu_share, sampled, wire_ops, SIMDS, HBM_PEAK_GBS  # noqa: E402
+from bench import cpu_share, sampled, wire_ops, measured_traffic, SIMDS, HBM_PEAK_GBS  # noqa: E402
 from fuzz_gen import config5_wire  # noqa: E402
 from oracle_lib import OracleDoc, lib as olib  # noqa: E402
 
@@ -134,7 +134,9 @@ print(json.dumps({
                "doc0": {"raw_entries": sizes0["raw"], "leaves": sizes0["leaves"], "double_deletes": sizes0["dd"],
                         "canonical_spans": sizes0["canon"], "len": sizes0["len"]}},
     "roofline": {"bound": "hbm", "achieved": alg / (rk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": alg / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None, "kernel": f"k_replay<{a.leaf}>",
+                 "frac": alg / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                 "traffic": measured_traffic(a.docs, "k_replay", "config5") if a.leaf == 32 else None,
+                 "traffic_file": "profiles/traffic_k_replay_config5.json", "kernel": f"k_replay<{a.leaf}>",
                  "kernel_ms": rk, "alg_bytes_per_launch": alg,
                  "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops)"},
     "kernels_ms": {"k_replay": rk, "k_publish": float(np.mean(pms))},

@@ -18,11 +18,25 @@ ap.add_argument("--local", action="store_true")
 ap.add_argument("--wire", default=None, help="a .rtx.gz remote wire file instead of a trace")
 ap.add_argument("--clean", action="store_true", help="reset and replay once more (single launch)")
 ap.add_argument("--random", type=int, default=0, help="config 4: this many generated ops per document")
+ap.add_argument("--config3", action="store_true",
+                help="config 3: mixed local corpus, document d replays trace splitmix64(d) %% 3 (shared record streams)")
+ap.add_argument("--no-share", action="store_true", help="config 3: one record stream copy per document")
 ap.add_argument("--config5", action="store_true",
                 help="config 5: one seeded concurrent history (1 M-char base, 16 agents x 64 rounds x 64 txns) on every document")
 a = ap.parse_args()
 e = crdt_amd.Engine(a.docs, 32)
-if a.config5:
+if a.config3:
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from bench import splitmix64
+    names = ["automerge-paper", "rustcode", "sveltecomponent"]
+    traces = [load_trace(x) for x in names]
+    which = np.array([splitmix64(d) % 3 for d in range(a.docs)], np.uint32)
+    if not a.no_share:
+        e.share_streams(True)
+    ag = e.agent_intern(list(range(a.docs)), ["jeremy"] * a.docs)
+    e.stage_local_shared(list(range(a.docs)), which, int(ag[0]), traces)
+elif a.config5:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fuzz_gen import config5_wire
     e.stage_remote_replicated(config5_wire(7, base_len=1 << 20, n_agents=16, rounds=64, ops=64), 0xFFFFFFFF, [""] * a.docs)

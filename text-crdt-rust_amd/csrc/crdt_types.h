@@ -281,6 +281,14 @@ struct DocState {
 // per word).  integrate's scan reads one row per leaf instead of one order -> agent map line per
 // entry; a commit of the leaf (or its creation) clears word 0, the scan rewrites a stale row.
 constexpr u32 lag_words(int L) { return L >= 16 ? (u32)L : 16u; }
+// The row's scan summary (written with it, current with it): word LAG_EPOCH = the agent count its
+// ranks are of (| LAG_MIXED when the entries' origin_left differ or the leaf is empty), LAG_OL =
+// the entries' common origin_left, LAG_RANK = their highest agent rank, [LAG_OMIN, LAG_OMAX] = the
+// range of their first orders.  integrate's scan passes a leaf with a summary of X / rank below
+// its own / orr outside the range unread (replay_core.h skip_leaves).
+enum : u32 { LAG_EPOCH = 1, LAG_OL = 4, LAG_RANK = 5, LAG_OMIN = 6, LAG_OMAX = 7 };
+constexpr u32 LAG_MIXED = 0x80000000u;
+static_assert(LAG_OMAX < lag_words(4) / 2, "summary words before the agent words");
 struct Pools {
   Span* leaves;        // [leaf][L]
   u32* dir_leaf;       // [blk*64 + i]

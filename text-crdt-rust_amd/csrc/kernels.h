@@ -105,8 +105,11 @@ __device__ __forceinline__ void replay_doc(Pools P, u32 n, u32 wpb, u32 rcap, co
   r.run();
   r.finish();
 }
+#ifndef CRDT_REPLAY_WAVES
+#define CRDT_REPLAY_WAVES 8  // waves per SIMD the replay's register budget is held to (diagnostic builds vary it)
+#endif
 template <int L>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRDT_REPLAY_WAVES))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
   replay_doc<L, false>(P, n, wpb, rcap, list);
 }
 // Documents past the LDS root replay with the two-level root (wave_gpu.h HR).  They are few and

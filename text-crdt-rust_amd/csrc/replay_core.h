@@ -554,6 +554,26 @@ struct Replayer {
     return (ka > kb) - (ka < kb);
   }
   CRDT_HD Cursor cursor_at_start() const { return Cursor{leaf_at_start(), 0, 0}; }  // root.rs:133-150
+  // integrate's scan (doc.rs:183-221) past whole leaves: the leaves after the cached one, in
+  // document order (directory block rows, 64 leaves per step), whose summary (crdt_types.h LAG_*)
+  // shows every entry passing the scan with no event -- origin_left X (a tie), agent rank below
+  // the new item's (scanning = false, go on), not orr -- are passed unread, as the sequential scan
+  // would pass them entry by entry.  Returns the first leaf that must be read (INVALID: none; the
+  // scan then runs off the end of the document, ST_NONTERMINATING as before).
+  CRDT_HD u32 skip_leaves(u32 X, u32 orr, u32 agent) {
+    u32 na = g(S_N_AGENTS), ng = g(S_NG);
+    u32 my_rank = w.rank_of(agents(), na, agent);
+    u32 blk = g(C_BLK), a = g(C_I) + 1u;
+    u32 gg = w.root_find_blk(ng, blk);
+    while (true) {
+      u32 cnt = w.root_cnt(gg), leaf;
+      u32 j = w.skip_scan(dleaf(blk), a, cnt, ptr<u32>(P_LAG), X, orr, my_rank, na, lv(), agents(), leaf);
+      if (j < cnt) return leaf;
+      if (++gg >= ng) return INVALID;
+      blk = w.root_blk(gg);
+      a = 0u;
+    }
+  }
   // root.rs:54-88 + 401-411, leaf.rs:61-84 (stick_end = false)
   CRDT_HD bool cursor_at_content_pos(u32 pos, Cursor& c) {
 #ifdef CRDT_PROF
@@ -972,18 +992,19 @@ struct Replayer {
     }
     if (q.lb >= nb) q = DDPos{nb - 1u, dd_cnt(nb - 1u)};  // the end: append to the last block
     DDBlk B = w.ld_ddblk(ddb() + q.lb);
-    if (B.cnt == DD_BLK) {
+    u32 bp = B.phys, bc = B.cnt;  // (two scalars, not the block record: no 4-register tuple to keep)
+    if (bc == DD_BLK) {
       if (nb >= g(K_DD)) return false;
       u32 np = nb;  // physical blocks are allocated in order
-      u32 first2 = w.dd_split(dd() + (u64)B.phys * DD_BLK, dd() + (u64)np * DD_BLK);
+      u32 first2 = w.dd_split(dd() + (u64)bp * DD_BLK, dd() + (u64)np * DD_BLK);
       w.ddb_insert(ddb(), nb, q.lb + 1u, DDBlk{np, first2, DD_BLK / 2u, 0u});
       w.st(&ddb()[q.lb].cnt, DD_BLK / 2u);
       p(S_N_DDB, nb + 1u);
-      if (q.i > DD_BLK / 2u) { q.lb += 1u; q.i -= DD_BLK / 2u; B = DDBlk{np, first2, DD_BLK / 2u, 0u}; }
-      else B.cnt = DD_BLK / 2u;
+      if (q.i > DD_BLK / 2u) { q.lb += 1u; q.i -= DD_BLK / 2u; bp = np; }
+      bc = DD_BLK / 2u;
     }
-    w.dd_block_insert(dd() + (u64)B.phys * DD_BLK, B.cnt, q.i, r);
-    w.st(&ddb()[q.lb].cnt, B.cnt + 1u);
+    w.dd_block_insert(dd() + (u64)bp * DD_BLK, bc, q.i, r);
+    w.st(&ddb()[q.lb].cnt, bc + 1u);
     if (q.i == 0u) w.st(&ddb()[q.lb].first, r.key);
     inc(S_N_DD);
     return true;
@@ -1335,7 +1356,7 @@ struct Replayer {
                 ag = w.lag_agents(lw, nn, oag(), tk_, tl_, ta_);
               } else {
                 ag = w.scan_gather(nn, oag());
-                if (clean) w.lag_store(lagp(c.leaf), ag, nn, tk_, tl_, ta_);
+                if (clean) w.lag_store(lagp(c.leaf), ag, nn, tk_, tl_, ta_, rt, na, agents());
               }
               u32 f = w.scan_batch(ag, rt, agent, c.idx, nn, item.ol, item.orr, agents(), na,
                                    tk_, tl_, ta_, last, last_scan);
@@ -1345,8 +1366,18 @@ struct Replayer {
               }
               if (f >= nn) {  // no event in this leaf: on to the next one (next_entry, cursor.rs:127-145)
                 if (pl == INVALID) return ST_NONTERMINATING;
-                switch_to_prefetched(pl, pslot, psucc);
-                c = Cursor{pl, 0u, 0u};
+                // ... past every following leaf whose summary shows it passes with no event
+                u32 jl = skip_leaves(item.ol, item.orr, agent);
+                CRDT_STAT(66, 1); CRDT_STAT(67, jl != pl);
+                if (jl == pl) {
+                  switch_to_prefetched(pl, pslot, psucc);
+                } else {
+                  if (jl == INVALID) return ST_NONTERMINATING;
+                  scanning = false;  // (every skipped entry ranks below the new item)
+                  w.prefetch_drain();
+                  ensure(jl);
+                }
+                c = Cursor{jl, 0u, 0u};
                 continue;
               }
               c.idx = f;

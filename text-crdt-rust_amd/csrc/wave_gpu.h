@@ -30,6 +30,18 @@ __device__ __forceinline__ u32 wrlane(u32 old, u32 v, u32 l) { return (u32)crdt_
 __device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ u32 shfl(u32 v, u32 src) { return __builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); }
 
+// Unsigned max / min over the wave (the DPP sequence of wave_or; lanes without a source take the
+// identity)
+__device__ __forceinline__ u32 wave_umax(u32 v) {
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));
+  v = max(v, (u32)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ u32 wave_umin(u32 v) { return ~wave_umax(~v); }
 // Inclusive wave64 prefix sum (LLVM AMDGPUAtomicOptimizer GFX9 sequence).
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
   v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
@@ -425,14 +437,47 @@ struct WaveGPU {
     return (l & 1u) ? v >> 16 : v & 0xFFFFu;
   }
   // ... and written from the gathered agents (the client_with_order tail run's orders are not in
-  // the map yet: their agent is the tail's), with word 0 = 1
-  __device__ __forceinline__ void lag_store(u32* p, u32 ag, u32 n, u32 tkey, u32 tlen, u32 tagent) const {
+  // the map yet: their agent is the tail's), with word 0 = 1, and the leaf's scan summary
+  // (crdt_types.h LAG_*): the agent count the ranks are of, the entries' common origin_left (or
+  // "mixed"), their highest agent rank and the range of their first orders
+  __device__ __forceinline__ void lag_store(u32* p, u32 ag, u32 n, u32 tkey, u32 tlen, u32 tagent, u32 rt, u32 n_agents,
+                                            const AgentRec* agents) const {
     u32 l = lane();
-    u32 o = l < n ? (u32)eo : rdlane(eo, 0);
+    bool in = l < n;
+    u32 o = in ? (u32)eo : rdlane(eo, 0);
     ag = o - tkey < tlen ? tagent : ag;
     u32 lo = shfl(ag, 2u * (l - lag_words(L) / 2u)), hi = shfl(ag, 2u * (l - lag_words(L) / 2u) + 1u);
     u32 v = l == 0u ? 1u : ((hi << 16) | (lo & 0xFFFFu));
-    if (l == 0u || (l >= lag_words(L) / 2u && l < lag_words(L) / 2u + (u32)L / 2u)) *(u32*)(p + l) = v;
+    u32 rk = n_agents <= RANK_LDS ? (u32)__builtin_amdgcn_ds_bpermute((int)(ag * 4u), (int)rt)
+                                  : *(const u32*)((const char*)agents + (u64)(ag * (u32)sizeof(AgentRec) + 12u));
+    u32 mr = wave_umax(in ? rk : 0u);
+    u32 omin = wave_umin(in ? o : 0xFFFFFFFFu), omax = wave_umax(in ? o : 0u);
+    u32 el0 = rdlane(el, 0);
+    u32 mixed = (n == 0u || ballot(in && el != el0) != 0ull) ? LAG_MIXED : 0u;
+    v = l == LAG_EPOCH ? (n_agents | mixed) : l == LAG_OL ? el0 : l == LAG_RANK ? mr : l == LAG_OMIN ? omin : l == LAG_OMAX ? omax : v;
+    if (l <= LAG_OMAX || (l >= lag_words(L) / 2u && l < lag_words(L) / 2u + (u32)L / 2u)) *(u32*)(p + l) = v;
+  }
+  // integrate's scan over whole leaves (replay_core.h skip_leaves): of the leaves in slots [a, cnt)
+  // of a directory leaf row, the first whose summary does not show that every entry passes the
+  // scan with no event -- a current row (of this launch's agent count) whose entries all have
+  // origin_left X, rank below my_rank and a first order other than orr.  Returns its slot (cnt:
+  // none) and its leaf id.
+  __device__ __forceinline__ u32 skip_scan(const u32* row, u32 a, u32 cnt, const u32* lag, u32 X, u32 orr, u32 my_rank,
+                                           u32 n_agents, const Span* leaves, const AgentRec* agents, u32& leaf) const {
+    (void)leaves; (void)agents;  // (the CPU emulation checks every skipped leaf against them)
+    u32 l = lane();
+    bool in = l >= a && l < cnt;
+    u32 lf = row[l];  // 64-slot row: always in bounds
+    // (32-bit byte offsets from the uniform base: saddr loads, one offset VGPR)
+    u32 off = (in ? lf : 0u) * (lag_words(L) * 4u);
+    uint2 h = *(const uint2*)((const char*)lag + (u64)off);                 // current flag, epoch
+    uint4 sm = *(const uint4*)((const char*)lag + (u64)(off + LAG_OL * 4u));  // origin_left, max rank, first-order range
+    bool skip = h.x == 1u && h.y == n_agents && sm.x == X && sm.y < my_rank && orr - sm.z > sm.w - sm.z;
+    u64 stop = ballot(in && !skip);
+    if (!stop) return cnt;
+    u32 j = (u32)__builtin_ctzll(stop);
+    leaf = rdlane(lf, j);
+    return j;
   }
   // the LDS rank table as one row (lane a: agent a's rank), read before an LDS-DMA is requested:
   // an LDS read issued after one waits for every outstanding load, the DMA's included
@@ -534,6 +579,8 @@ struct WaveGPU {
     u32 l = lane();
     if (l < (u32)L) __builtin_amdgcn_global_load_lds((g_u32*)(p + l), pf, 16, 0, 0);
   }
+  // a requested successor the scan does not take (skip_leaves): its LDS-DMA completes first
+  __device__ __forceinline__ void prefetch_drain() const { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
   __device__ __forceinline__ u32 cache_from_prefetch() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the DMA counts in vmcnt; it is not a VGPR the compiler tracks)
     u32 l = lane();
