@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/micro
 D=${DOCS:-2048}
 TAG=${TAG:-}
-for W in base typing jump10 jump1 bs10 del1; do
+for W in ${WLS:-base typing jump10 jump1 bs10 del1 bs200 fd200}; do
   timeout -s KILL 120 rocprofv3 --kernel-include-regex k_replay --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_LDS SQ_WAVES SQ_INSTS_BRANCH \
     -d gpurun_out/micro/$W$TAG -o m --output-format csv -- python scripts/prof_replay.py --docs $D --clean --wire data/micro/$W.rtx.gz > gpurun_out/micro/$W$TAG.log 2>&1 || exit 1
   echo $W-ok

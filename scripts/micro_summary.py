@@ -26,7 +26,7 @@ base, bns = load("base")
 print(f"{'workload':8s} {'all':>7s} " + " ".join(f"{k[9:].lower():>8s}" for k in KEYS) + "   ns/op(launch)")
 b = {k: base.get(k, 0) / docs for k in KEYS}
 print(f"{'base/op':8s} {sum(b.values()) / 50000:7.1f} " + " ".join(f"{b[k] / 50000:8.1f}" for k in KEYS) + f"   {bns / 50000:.1f}")
-for w in ("typing", "jump10", "jump1", "bs10", "del1"):
+for w in ("typing", "jump10", "jump1", "bs10", "del1", "bs200", "fd200"):
     a, ns = load(w)
     d = {k: (a.get(k, 0) - base.get(k, 0)) / docs / N for k in KEYS}
     print(f"{w:8s} {sum(d.values()):7.1f} " + " ".join(f"{d[k]:8.1f}" for k in KEYS) + f"   {(ns - bns) / N:.1f}")

@@ -35,11 +35,17 @@ def workload(kind: str, seed: int = 1):
             p = int(rng.integers(1, length))
             pats += [(p + i, 0, 1) for i in range(run)]
             length += run
-    elif kind in ("bs10", "del1"):
-        run = 10 if kind == "bs10" else 1
+    elif kind in ("bs10", "del1", "bs200"):
+        run = {"bs10": 10, "del1": 1, "bs200": 200}[kind]
         for _ in range(N // run):
             p = int(rng.integers(run, length))
             pats += [(p - i, 1, 0) for i in range(run)]  # backspace: each deletes the char before
+            length -= run
+    elif kind == "fd200":  # forward delete runs: each deletes the char at the same position
+        run = 200
+        for _ in range(N // run):
+            p = int(rng.integers(0, length - run))
+            pats += [(p, 1, 0) for i in range(run)]
             length -= run
     elif kind != "base":
         raise ValueError(kind)
@@ -48,11 +54,11 @@ def workload(kind: str, seed: int = 1):
     return counts, patches
 
 
-KINDS = ("base", "typing", "jump10", "jump1", "bs10", "del1")
+KINDS = ("base", "typing", "jump10", "jump1", "bs10", "del1", "bs200", "fd200")
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    for k in KINDS:
+    for k in (sys.argv[1:] or KINDS):
         c, p = workload(k)
         w = trace_to_wire(c, p, "jeremy")
         loc = OracleDoc()
