@@ -30,6 +30,9 @@ elif mode == "config5":  # one seeded concurrent history (SURVEY 8(d) shape) on 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fuzz_gen import config5_wire
     e.stage_remote_replicated(config5_wire(7, base_len=1 << 20, n_agents=16, rounds=64, ops=64), 0xFFFFFFFF, [""] * n)
+elif mode.startswith("wire:"):  # a remote wire file (e.g. data/micro/fd200.rtx.gz) on every document
+    import gzip
+    e.stage_remote_replicated(gzip.open(os.path.join(ROOT, mode[5:]), "rb").read(), 0, ["u%05d" % i for i in range(n)])
 elif local:
     t = load_trace("automerge-paper")
     ag = e.agent_intern(list(range(n)), ["jeremy"] * n)

@@ -5,6 +5,7 @@
 #ifdef CRDT_EMU_STATS  // statistics build (make stats): event counters of replay_core.h's CRDT_STAT sites
 static unsigned long long g_stat[128];
 #define CRDT_STAT(k, v) (g_stat[(k)] += (unsigned long long)(v))
+#define WCPU_COUNT(kind, f) (g_stat[124 + (kind > 3 ? 3 : kind)]++)  // (context reads / writes / cache reads / other)
 #endif
 #include <cstdio>
 #include <cstdlib>

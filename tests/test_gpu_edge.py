@@ -356,3 +356,24 @@ def test_config4_batches_reseed_and_fit_note():
     from bench import splitmix64
     assert o.apply_random(o.agent("gen"), ops, splitmix64(seed ^ (2 * n + 5)) & 0xFFFFFFFF) == 0
     assert int(want[2 * n + 5]) == o.digest()
+
+
+def test_fitted_forward_delete_runs():
+    # forward-delete runs (the delete key held down: data/micro/fd200, 200-delete runs at random
+    # places of a 50,000-char document) replayed in fitted capacities (crdt_fit: the delete log's
+    # room is the stream's own count) take the fast path's room check for one coalesced log run and
+    # reach the same state as the oracle
+    import gzip
+    import os
+    w = gzip.open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data", "micro", "fd200.rtx.gz"), "rb").read()
+    o = OracleDoc()
+    assert o.apply_remote_wire(w) == 0
+    e = crdt_amd.Engine(4, 32)
+    assert (e.apply_remote_wire([0, 1, 2, 3], [w] * 4) == 0).all()
+    e.fit()
+    e.reset_async()
+    e.run_async()
+    e.sync()
+    assert (e.status() == 0).all()
+    assert (e.digests() == np.uint64(o.digest())).all()
+    assert_same(e.export(2), o.export())

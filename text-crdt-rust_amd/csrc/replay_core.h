@@ -1804,7 +1804,10 @@ struct Replayer {
 
 #endif
     if (g(K_MAP) - first < k * l) return 0;
-    if (g(K_DEL) - g(S_N_DEL) < k) return 0;
+    // delete-log room: a backspace run logs one run per item, a forward run coalesces into one
+    // (was k for both: after crdt_fit the log's room is the stream's own count, so every forward
+    // run of a fitted document took the general path)
+    if (g(K_DEL) - g(S_N_DEL) < (back ? k : 1u)) return 0;
 #ifdef CRDT_PROF
     u64 pt1 = w.clock();
 #endif
@@ -2107,7 +2110,7 @@ struct Replayer {
     u32 kl, ol;
     if (!w.cfind_content(n, rem + l - 1u, kl, ol)) return 0;
     if (kl >= n) return 0;
-    if (g(K_DEL) - g(S_N_DEL) < l) return 0;  // (one delete run per deactivated piece at most)
+    if (g(K_DEL) - g(S_N_DEL) < (l < (u32)L ? l : (u32)L)) return 0;  // (one delete run per deactivated piece at most: <= L pieces)
     if (g(K_MAP) - first < l) return 0;
     u32 rl = ol + 1u;  // items deleted from entry kl
     // the pieces insert_internal places, and whether each prepends onto the entry after it
