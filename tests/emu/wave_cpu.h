@@ -124,6 +124,9 @@ struct WaveCPU {
   void cset(u32 i, const Span& s) { WCPU_COUNT(4, 0); c[i & 63] = s; }
   void cset_len(u32 i, i32 len) { c[i & 63].len = len; }
   template <class F> void cset_lanes(u32 a, u32 b, F f) { for (u32 l = a; l < b && l < 64; l++) c[l] = f(l); }
+  template <class F> void leaf_write_lanes(Span* dst, u32 n, F f) const {
+    for (u32 l = 0; l < (u32)L; l++) dst[l] = l < n ? f(l) : Span{0, 0, 0, 0};
+  }
   u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
   void rank_load(const AgentRec*, u32) const {}
   u32 rank_of(const AgentRec* agents, u32, u32 a) const { return agents[a].rank; }

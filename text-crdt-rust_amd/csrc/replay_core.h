@@ -682,7 +682,19 @@ struct Replayer {
     p(C_NOW, g(C_NOW) - stolen);
     p(C_N, idx);
     p(C_DIRTY, 1u);
-    // link nl right after the cached leaf (directory block insert; the block splits when full)
+    dir_link(rl, rv, blk, i, nl, stolen, extra_vis);
+    p(C_SUCC, nl);
+    p(C_SUCC_ORD, padding ? INVALID : first_moved);  // (padding: the caller writes nl's first entries)
+#ifdef CRDT_PROF
+    prof_split += (u32)(w.clock() - psa);
+#endif
+    return nl;
+  }
+  // Link leaf nl right after the cached leaf (slot i of block blk, whose directory rows rl / rv
+  // were requested by the caller): a directory block insert; the block splits when full.  The
+  // cached leaf's slot loses `stolen` visible items (moved to nl); the group's visible total
+  // changes only by extra_vis (items the caller placed in nl itself).
+  CRDT_HD void dir_link(u32 rl, u32 rv, u32 blk, u32 i, u32 nl, u32 stolen, u32 extra_vis) {
     u32 ng = g(S_NG);
     u32 gg = w.root_find_blk(ng, blk);
     u32 cnt = w.root_cnt(gg);
@@ -699,8 +711,6 @@ struct Replayer {
       }
       cnt = 32;
     }
-    // the cached leaf's slot loses `stolen` (moved to nl, the next slot); the group's visible
-    // total changes only by extra_vis
     u32 cv = g(C_VIS) - stolen;
     w.blk_insert_at(rl, rv, dleaf(blk), dvis(blk), cnt, i, cv, nl, stolen + extra_vis, sol(), blk);
     w.root_set_cnt(gg, cnt + 1u);
@@ -709,12 +719,70 @@ struct Replayer {
       inc(S_LEN, extra_vis);
     }
     p(C_VIS, cv);
-    p(C_SUCC, nl);
-    p(C_SUCC_ORD, padding ? INVALID : first_moved);  // (padding: the caller writes nl's first entries)
-#ifdef CRDT_PROF
-    prof_split += (u32)(w.clock() - psa);
-#endif
-    return nl;
+  }
+  // A backspace run inside visible entry E (idx) of the cached leaf, right after a leaf split, in
+  // closed form over whole leaves.  In a full leaf every delete_general splits at idx + 1; from
+  // then on the run repeats one cycle -- fill the leaf after E (delete_run_closed: pieces of two
+  // deleted items each), then split it again -- so each cycle is a new leaf of known entries linked
+  // right after the cached leaf, and E shrinks by the cycle's deletes:
+  //  * follow split (idx + 1 >= L/2: the pieces of the splitting delete go to the new leaf; the
+  //    cached leaf is [0, idx]): cycle of 2r + 1 deletes, r = L - idx - 1; for first target t the
+  //    new leaf is [{t-2r, t-2r-1, -1}, {t-2r+1, t-2r+1, -2}, ..., {t-1, t-1, -2}];
+  //  * otherwise (the split leaves [0, idx] + D = {t+1, t, -1} in the cached leaf): the cycle's
+  //    first delete prepends onto D (span.rs:61-64 keeps D's origin_left), 2r more fill the leaf
+  //    (r = L - idx - 2), and the splitting delete stays in the cached leaf as the next D: cycle of
+  //    2r + 2 deletes, new leaf [{t-2r, t-2r, -2}, {t-2r+2, t-2r+2, -2}, ..., {t, t, -2}].
+  // (mutations.rs:520-570 mutate_entry + :17-179 insert_internal + :623-669 split_at, op by op,
+  // give the same leaves; the CPU emulation runs both.)  All entries share E's origin_right.
+  // t: the run's next target (E's last item), rem: deletes left.  Returns the deletes applied (0:
+  // not this state).
+  CRDT_HD u32 back_cycles(u32 idx, u32 t, u32 rem) {
+    u32 n = g(C_N);
+    Span E = w.cget(idx);
+    u32 follow = idx + 1u == n ? 1u : 0u;
+    if (!follow) {  // [.., E, D] with D the run's last deleted item
+      if (idx + 2u != n) return 0;
+      Span D = w.cget(idx + 1u);
+      if (D.order != t + 1u || D.ol != t || D.len != -1 || D.orr != E.orr) return 0;
+    }
+    if (E.len <= 0 || E.order + (u32)E.len - 1u != t) return 0;
+    // (follow is the split's own rule: a split at idx + 1 >= L/2 moves the pieces with the new leaf)
+    if (follow != (idx + 1u >= (u32)L / 2u ? 1u : 0u)) return 0;
+    u32 r = (u32)L - n, per = 2u * r + 1u + (follow ^ 1u);
+    u32 cyc = rem / per, c2 = ((u32)E.len - 1u) / per, c3 = g(K_LEAF) - g(S_N_LEAVES);
+    cyc = cyc < c2 ? cyc : c2;
+    cyc = c3 < 2u ? 0u : (cyc < c3 - 2u ? cyc : c3 - 2u);
+    if (cyc == 0u) return 0;
+    u32 orr = E.orr;
+    for (u32 q = 0; q < cyc; q++) {
+      u32 blk = g(C_BLK), i = g(C_I);
+      u32 rl = w.row_ld(dleaf(blk)), rv = w.row_ld(dvis(blk));  // (dir_link's rows, requested first)
+      u32 nl = g(S_N_LEAVES);
+      p(S_N_LEAVES, nl + 1);
+      u32 osucc = cached_succ_leaf();
+      w.st(w.template at<2>(sol(), nl) + 1, osucc == INVALID ? END_LEAF : osucc);
+      w.st(w.template at<2>(sol(), g(C_LEAF)) + 1, nl);
+      u32 base = t - 2u * r;  // the new leaf's first order (its items are [base, base + per - ...])
+      w.leaf_write_lanes(leafp(nl), r + 1u, [&](u32 lane) {
+        u32 o = follow ? base + 2u * lane - 1u : base + 2u * lane;
+        u32 first = follow & (lane == 0u ? 1u : 0u);
+        return Span{first ? base : o, first ? base - 1u : o, orr, first ? -1 : -2};
+      });
+      lag_stale(nl);
+      map_fill(base, follow ? 2u * r + 1u : 2u * r + 2u, nl);  // notify (doc.rs:143-153)
+      dir_link(rl, rv, blk, i, nl, 0u, 0u);
+      p(C_SUCC, nl);
+      p(C_SUCC_ORD, base);
+      inc(S_N_ENTRIES, r + 1u);
+      t -= per;
+    }
+    u32 done = cyc * per;
+    E.len -= (i32)done;
+    w.cset(idx, E);
+    if (!follow) w.cset(idx + 1u, Span{t + 1u, t, orr, -1});
+    p(C_NOW, g(C_NOW) - done);
+    p(C_DIRTY, 1u);
+    return done;
   }
   // mutations.rs:17-179 insert_internal.  Items a0..a(n-1) (n <= 3) stay in named registers;
   // home: the leaf the items already live in (INVALID for fresh orders), for notify().
@@ -1868,6 +1936,17 @@ struct Replayer {
       u64 q3 = w.clock();
       lp_find += (u32)(q3 - q2);
 #endif
+      // the split left the run in its repeating state: whole cycles in closed form
+      if (back & (c.leaf == g(C_LEAF)) & (l == 1u)) {
+        u32 dc = back_cycles(c.idx, t2, k - done);
+        CRDT_STAT(57, dc != 0u); CRDT_STAT(58, dc);
+        if (dc) {
+          done += dc;
+          if (done == k) break;
+          t2 -= dc;
+          c.off -= dc;
+        }
+      }
       u32 dseg = delete_segment(c.idx, c.off, t2, k - done, back, l);
 #ifdef CRDT_PROF_LOOP
       lp_seg += (u32)(w.clock() - q3);

@@ -571,6 +571,13 @@ struct WaveGPU {
     if (l < (u32)L) *(uint4*)(dst + l) = make_uint4(mo, ml, mr, mn);
   }
   __device__ __forceinline__ void cache_from_moved() { eo = mo; el = ml; er = mr; en = (i32)mn; }
+  // a new leaf's entries [0, n) := f(lane), the rest empty: computed lane-parallel, one store
+  template <class F> __device__ __forceinline__ void leaf_write_lanes(Span* dst, u32 n, F f) const {
+    u32 l = lane();
+    Span e = f(l);
+    bool in = l < n;
+    if (l < (u32)L) *(uint4*)(dst + l) = in ? make_uint4(e.order, e.ol, e.orr, (u32)e.len) : make_uint4(0, 0, 0, 0);
+  }
   // A leaf requested ahead into this wave's LDS row by LDS-DMA (global_load_lds_dwordx4: lane l's
   // entry to row + 16 l, no VGPR holds it in flight), made the cached leaf once integrate's scan
   // reaches it (returns its entry count).
