@@ -143,3 +143,26 @@ def test_bench_without_gpus_fails_cleanly():
                        capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode != 0
     assert "need 2 GPU(s)" in r.stderr
+
+
+@pytest.mark.parametrize("gpus", [1, 2, 8])
+def test_bench_config4_corpus_rehearsal(gpus):
+    # `bench.py --gpus N --workload config4`: the 1 M-document corpus sharded into contiguous
+    # ranges of 1 M / N, each rank's share in batches of <= 125,000; the rehearsal checks that the
+    # shards and the gather cover every corpus document exactly once, in order
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--rehearse-cpu",
+                        "--workload", "config4"], capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][0])
+    assert out["parity_ok"] and out["docs_total"] == 1_000_000 and out["world_size"] == gpus
+    assert out["shards"] == [[k * (1_000_000 // gpus), 1_000_000 // gpus] for k in range(gpus)]
+    assert out["batches_per_rank"] == 8 // gpus and out["batch_docs"] == 125_000
+
+
+def test_config4_batches_cover_a_ragged_share():
+    import bench
+    B, batches = bench.config4_batches(10, 333_334, 125_000)
+    assert B == 111_112 and [m for _, m in batches] == [111_112, 111_112, 111_110]
+    assert batches[0][0] == 10 and batches[-1][0] + batches[-1][1] == 10 + 333_334

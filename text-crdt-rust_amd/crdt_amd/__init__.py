@@ -208,6 +208,16 @@ def lib():
     if not os.path.exists(path):
         raise CrdtError(f"{path} not built (run __graft_entry__.build())")
     L = C.CDLL(path)
+    if path != LIB_PATH:  # a diagnostic library from an older tree may lack later entry points
+        class _Missing:
+            def __init__(self, name):
+                self.name = name
+
+            def __call__(self, *a):
+                raise CrdtError(f"{self.name}: not in {path}")
+        for name in EXPORTED_SYMBOLS:
+            if not hasattr(L, name):
+                setattr(L, name, _Missing(name))
     vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int32
     P = C.POINTER
 
