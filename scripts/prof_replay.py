@@ -17,6 +17,8 @@ ap.add_argument("--trace", default="automerge-paper")
 ap.add_argument("--local", action="store_true")
 ap.add_argument("--wire", default=None, help="a .rtx.gz remote wire file instead of a trace")
 ap.add_argument("--clean", action="store_true", help="reset and replay once more (single launch)")
+ap.add_argument("--no-fit", action="store_true", help="keep the growth capacities (as bench_config3.py; an older "
+                "library's fit may not fit memory)")
 ap.add_argument("--random", type=int, default=0, help="config 4: this many generated ops per document")
 ap.add_argument("--config3", action="store_true",
                 help="config 3: mixed local corpus, document d replays trace splitmix64(d) %% 3 (shared record streams)")
@@ -57,7 +59,8 @@ t0 = time.time()
 st = e.run()
 e.publish_async()
 e.sync()
-e.fit()  # as bench.py: capacities = the stream's use
+if not a.no_fit:
+    e.fit()  # as bench.py: capacities = the stream's use
 replay_ms = e.timings()[0]  # (the growth loop's last launch: without --clean not a full replay)
 if a.clean:
     import ctypes as C

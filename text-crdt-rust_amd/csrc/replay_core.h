@@ -152,7 +152,9 @@ struct Replayer {
   // a leaf's agent row is no longer current (its entries change, or it is new).  (Every document
   // has the rows; only documents that read them store: a lane predicate, where a branch on
   // K_AGMAP at every commit cost the register budget.)
-  CRDT_HD void lag_stale(u32 leaf) { w.st_lanes(lagp(leaf), 0u, g(K_AGMAP)); }
+  CRDT_HD void lag_stale(u32 leaf) {
+    if (g(K_AGMAP)) w.st(lagp(leaf), 0u);  // (a uniform branch: local-only documents skip the address too)
+  }
   CRDT_HD CwoRun* cwo() const { return ptr<CwoRun>(P_CWO); }
   CRDT_HD ARun* arun() const { return ptr<ARun>(P_ARUN); }
   CRDT_HD DelRun* dels() const { return ptr<DelRun>(P_DELS); }
