@@ -4,8 +4,8 @@ Per document: agent "base" inserts a 1M-char run (one txn), then 16 agents x 64 
 single-op txns against the round-start snapshot (60 % deletes of 1..64 base items -> double
 deletes, 40 % 1..8-char inserts at 32 shared hotspots -> integrate's Equal-branch ties), delivered
 in a per-document seeded interleaving (tests/fuzz_gen.py config5_wire).  `--distinct` seeded
-histories are generated on the host and document d replays history d % distinct from its own
-device copy of the records.  One step = reset + replay (k_replay) + publish.
+histories are generated on the host and document d replays history d % distinct (the documents of
+one history read one device copy of its records).  One step = reset + replay (k_replay) + publish.
 
 Parity: every document's digest equals the oracle's replay of its history (the oracle is the
 checker and the CPU baseline).  Roofline: SURVEY §8(d) algorithmic bytes = docs x (32 B x
@@ -51,6 +51,8 @@ doc_w = [d % a.distinct for d in range(a.docs)]
 total_ops = sum(ops_of[k] for k in doc_w)
 
 e = crdt_amd.Engine(a.docs, a.leaf)
+# documents of one history read one device copy of its records (read-only during the replay)
+e.share_streams(True)
 t0 = time.time()
 e.apply_remote_wire(list(range(a.docs)), [wires[k] for k in doc_w], stage_only=True)
 stage_s = time.time() - t0
@@ -130,7 +132,7 @@ print(json.dumps({
     "config": {"workload": f"config5: {a.docs} docs/GPU x ({a.base}-char base + {a.agents} agents x {a.rounds} rounds x "
                            f"{a.ops} txns), replay+publish", "docs_per_gpu": a.docs, "distinct_histories": a.distinct,
                "ops_per_doc": ops_of[0], "leaf_cap": a.leaf, "waves_per_simd": a.docs / SIMDS,
-               "hbm_bytes_per_doc": mem / a.docs, "hbm_bytes": mem,
+               "hbm_bytes_per_doc": mem / a.docs, "hbm_bytes": mem, "device_peak_bytes": crdt_amd.Engine.device_bytes()[1],
                "doc0": {"raw_entries": sizes0["raw"], "leaves": sizes0["leaves"], "double_deletes": sizes0["dd"],
                         "canonical_spans": sizes0["canon"], "len": sizes0["len"]}},
     "roofline": {"bound": "hbm", "achieved": alg / (rk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -377,3 +377,30 @@ def test_fitted_forward_delete_runs():
     assert (e.status() == 0).all()
     assert (e.digests() == np.uint64(o.digest())).all()
     assert_same(e.export(2), o.export())
+
+
+def test_same_wire_staged_once_and_fit_keeps_exact_maps():
+    # documents handed one wire buffer stage one host stream (crdt_stage_remote_wire), referenced
+    # by one device copy with shared streams; crdt_fit sizes the order maps to next_order + 1 (a
+    # replay from reset checks next_order + txn_len <= map_cap per txn), and a relayout leaves the
+    # pools whose capacities did not change where they are.  Digests equal the oracle's before and
+    # after the fit, and a replay of the fitted engine needs no growth.
+    w, _ = concurrent_wire(11, n_agents=6, rounds=10, ops_per_round=6)
+    o = OracleDoc()
+    assert o.apply_remote_wire(w) == 0
+    for share in (False, True):
+        e = crdt_amd.Engine(6, 32)
+        e.share_streams(share)
+        assert (e.apply_remote_wire(list(range(6)), [w] * 6) == 0).all()
+        assert (e.digests() == np.uint64(o.digest())).all()
+        b0 = e.mem_bytes()
+        e.fit()
+        assert e.mem_bytes() <= b0
+        for _ in range(2):
+            e.reset_async()
+            e.run_async()
+            e.sync()
+            assert (e.status() == 0).all()
+            assert (e.digests() == np.uint64(o.digest())).all()
+        assert_same(e.export(5), o.export())
+        check_queries(e, 5, o)

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -54,6 +55,12 @@ hipError_t dalloc(T*& p, u64 n) {
     g_mem_peak = std::max(g_mem_peak, g_mem_cur);
   }
   return e;
+}
+// bytes of a live dalloc allocation (0 for anything else)
+u64 dsize(const void* p) {
+  std::lock_guard<std::mutex> g(g_mem_mu);
+  auto it = g_mem_size.find(const_cast<void*>(p));
+  return it == g_mem_size.end() ? 0 : it->second;
 }
 template <class T>
 void dfree(T*& p) {
@@ -437,8 +444,25 @@ struct crdt_engine {
     }
     HIPCHK(hipMemcpyAsync(segs, nseg.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
     // Pool by pool: allocate the new one, move every document's part (k_relayout_pool), free the
-    // old one.  The peak is the old pools + the largest new pool (2x both sets before).
-    auto step = [&](auto& old_p, auto& new_p, u64 count, u32 which) -> int {
+    // old one.  The peak is the old pools + the largest new pool (2x both sets before).  A pool
+    // whose every document keeps its capacity (so its base: bases are prefix sums) and whose
+    // element count is unchanged stays where it is -- growth of one table, or crdt_fit of a
+    // config-5 corpus whose order maps are already exact, then moves no order map (the largest
+    // pools) and the peak is lower by that much.
+    auto same_caps = [&](u32 DocSeg::*cap) {
+      if (!move) return false;
+      for (u64 d = 0; d < n_docs; d++)
+        if (nseg[d].*cap != seg_h[d].*cap) return false;
+      return true;
+    };
+    const bool s_leaf = same_caps(&DocSeg::leaf_cap), s_blk = same_caps(&DocSeg::blk_cap), s_map = same_caps(&DocSeg::map_cap),
+               s_cwo = same_caps(&DocSeg::cwo_cap), s_del = same_caps(&DocSeg::del_cap), s_dd = same_caps(&DocSeg::dd_cap),
+               s_txn = same_caps(&DocSeg::txn_cap), s_par = same_caps(&DocSeg::par_cap), s_fr = same_caps(&DocSeg::fr_cap);
+    auto step = [&](auto& old_p, auto& new_p, u64 count, u32 which, bool same = false) -> int {
+      if (move && same && old_p && dsize(old_p) == sizeof(*old_p) * std::max<u64>(count, 1)) {
+        new_p = nullptr;  // (stays: same bases, same size)
+        return 0;
+      }
       HIPCHK(dalloc(new_p, count));
       if (move && which < RL_N) {
         Pools src = pools_view(pools), dst = pools_view(pools);
@@ -454,24 +478,24 @@ struct crdt_engine {
       return 0;
     };
     r = 0;
-    if (!r) r = step(pools.leaves, np.leaves, nl * L, RL_LEAVES);
-    if (!r) r = step(pools.sol, np.sol, 2 * nl, RL_SOL);  // {directory slot, successor leaf} per leaf
-    if (!r) r = step(pools.dir_leaf, np.dir_leaf, nb * GROUP, RL_DIR_LEAF);
-    if (!r) r = step(pools.dir_vis, np.dir_vis, nb * GROUP, RL_DIR_VIS);
-    if (!r) r = step(pools.leaf_of, np.leaf_of, nm, RL_LEAF_OF);
-    if (!r) r = step(pools.agent_of, np.agent_of, n_agent_of, RL_AGENT_OF);
-    if (!r) r = step(pools.lag, np.lag, n_lag, RL_N);  // (not moved: every row starts stale)
+    if (!r) r = step(pools.leaves, np.leaves, nl * L, RL_LEAVES, s_leaf);
+    if (!r) r = step(pools.sol, np.sol, 2 * nl, RL_SOL, s_leaf);  // {directory slot, successor leaf} per leaf
+    if (!r) r = step(pools.dir_leaf, np.dir_leaf, nb * GROUP, RL_DIR_LEAF, s_blk);
+    if (!r) r = step(pools.dir_vis, np.dir_vis, nb * GROUP, RL_DIR_VIS, s_blk);
+    if (!r) r = step(pools.leaf_of, np.leaf_of, nm, RL_LEAF_OF, s_map);
+    if (!r) r = step(pools.agent_of, np.agent_of, n_agent_of, RL_AGENT_OF, s_map);
+    if (!r) r = step(pools.lag, np.lag, n_lag, RL_N, s_leaf);  // (not moved: every row starts stale)
     if (!r) HIPCHK(hipMemsetAsync(pools.lag, 0, n_lag * 4, stream));
     if (!r) r = step(pools.hrows, np.hrows, n_hrows, RL_N);  // (rebuilt from the groups at every launch)
     if (!r) r = step(pools.gsob, np.gsob, n_gsob, RL_N);
-    if (!r) r = step(pools.cwo, np.cwo, nc, RL_CWO);
-    if (!r) r = step(pools.dels, np.dels, ndl, RL_DELS);
-    if (!r) r = step(pools.dd, np.dd, ndd * DD_BLK, RL_DD);
-    if (!r) r = step(pools.ddb, np.ddb, ndd, RL_DDB);
-    if (!r) r = step(pools.txns, np.txns, nt, RL_TXNS);
-    if (!r) r = step(pools.parents, np.parents, npar, RL_PARENTS);
-    if (!r) r = step(pools.frontier, np.frontier, nfr, RL_FRONTIER);
-    if (!r) r = step(pools.groups, np.groups, nb, RL_GROUPS);
+    if (!r) r = step(pools.cwo, np.cwo, nc, RL_CWO, s_cwo);
+    if (!r) r = step(pools.dels, np.dels, ndl, RL_DELS, s_del);
+    if (!r) r = step(pools.dd, np.dd, ndd * DD_BLK, RL_DD, s_dd);
+    if (!r) r = step(pools.ddb, np.ddb, ndd, RL_DDB, s_dd);
+    if (!r) r = step(pools.txns, np.txns, nt, RL_TXNS, s_txn);
+    if (!r) r = step(pools.parents, np.parents, npar, RL_PARENTS, s_par);
+    if (!r) r = step(pools.frontier, np.frontier, nfr, RL_FRONTIER, s_fr);
+    if (!r) r = step(pools.groups, np.groups, nb, RL_GROUPS, s_blk);
     if (!r) r = step(pools.arun, np.arun, na, RL_ARUN);
     if (r) return r;
     if (move) {  // the agents' run counts and last-run copies into the new table
@@ -933,7 +957,9 @@ struct crdt_engine {
       c.txn = s.n_txn + 1;
       c.del = s.n_del + m.max_del + 1;
       c.par = s.n_par + std::max<u32>(m.max_parents, s.n_fr) + 64;
-      if (h.tracked) c.map = (u32)std::min<u64>((u64)s.next_order + m.max_len + 1, 0xFFFFFFFFull);
+      // (every txn checks map room for its own orders, next_order + txn_len <= map_cap, and orders
+      // only grow: the final next_order bounds every check of a replay from reset)
+      if (h.tracked) c.map = (u32)std::min<u64>((u64)s.next_order + 1, 0xFFFFFFFFull);
       c.ord = s.next_order + 1;
       c.canon = std::max<u32>(cn[d], 1);
       c.fr = std::max<u32>(s.n_fr + 1, FRONTIER_CAP0);
@@ -1421,6 +1447,10 @@ int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs
   std::vector<std::vector<Rec>> streams(n_docs);
   std::vector<StreamNeeds> needs(n_docs);
   std::vector<const std::vector<Rec>*> sp(n_docs);
+  // documents handed the same wire buffer whose encoding comes out identical (same name -> agent
+  // ids) stage one host stream: stage() then copies it on the device (or, with shared streams,
+  // references one device copy)
+  std::map<std::pair<const uint8_t*, uint64_t>, uint64_t> first_of;
   for (uint64_t i = 0; i < n_docs; i++) {
     if (docs[i] >= e->n_docs) return CRDT_E_ARG;
     ids[i] = docs[i];
@@ -1428,6 +1458,14 @@ int crdt_stage_remote_wire(crdt_engine* e, uint64_t n_docs, const uint32_t* docs
     if (!wv.parse(wire[i], wire_len[i])) return CRDT_E_WIRE;
     encode_remote(streams[i], needs[i], e->docs[docs[i]].agents, wv);
     sp[i] = &streams[i];
+    auto f = first_of.emplace(std::make_pair(wire[i], wire_len[i]), i);
+    if (!f.second) {
+      const std::vector<Rec>& a = streams[f.first->second];
+      if (a.size() == streams[i].size() && std::memcmp(a.data(), streams[i].data(), a.size() * sizeof(Rec)) == 0) {
+        sp[i] = &a;
+        std::vector<Rec>().swap(streams[i]);
+      }
+    }
   }
   return e->stage(ids, sp, needs);
 }
