@@ -24,7 +24,7 @@ ap.add_argument("--config3", action="store_true",
                 help="config 3: mixed local corpus, document d replays trace splitmix64(d) %% 3 (shared record streams)")
 ap.add_argument("--no-share", action="store_true", help="config 3: one record stream copy per document")
 ap.add_argument("--config5", action="store_true",
-                help="config 5: one seeded concurrent history (1 M-char base, 16 agents x 64 rounds x 64 txns) on every document")
+                help="config 5: bench_config5.py's 8 seeded concurrent histories (1 M-char base, 16 agents x 64 rounds x 64 txns)")
 a = ap.parse_args()
 e = crdt_amd.Engine(a.docs, 32)
 if a.config3:
@@ -41,7 +41,11 @@ if a.config3:
 elif a.config5:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fuzz_gen import config5_wire
-    e.stage_remote_replicated(config5_wire(7, base_len=1 << 20, n_agents=16, rounds=64, ops=64), 0xFFFFFFFF, [""] * a.docs)
+    # scripts/bench_config5.py's workload: 8 seeded histories, document d replays history d % 8,
+    # the documents of one history reading one device copy of its records
+    wires = [config5_wire(900 + s, base_len=1 << 20, n_agents=16, rounds=64, ops=64) for s in range(8)]
+    e.share_streams(True)
+    e.apply_remote_wire(list(range(a.docs)), [wires[d % 8] for d in range(a.docs)], stage_only=True)
 elif a.random:
     e.stage_random(list(range(a.docs)), "gen", a.random, 0xC0FFEE)
 elif a.local:

@@ -602,11 +602,21 @@ struct crdt_engine {
       return CRDT_E_NOMEM;
     }
     auto rc = [&](u32 k) { return k < 4 ? ROOT_CLASSES[k] : hr_top; };
+    // Within a class the longest staged streams launch first (LPT order): a workgroup's waves hold
+    // their slots until its last one ends, so workgroups of similar documents, longest first, leave
+    // the short ones to fill the end of the launch (mixed corpora: config 3).  Equal streams keep
+    // the document order (stable sort).
+    auto work = [&](u32 d) { return docs[d].staged.n_ops + docs[d].staged.n_txn; };
+    bool identity = true;
+    for (auto& v : by) {
+      std::stable_sort(v.begin(), v.end(), [&](u32 a, u32 b) { return work(a) > work(b); });
+      for (size_t i = 1; i < v.size(); i++) identity &= v[i] == v[i - 1] + 1u;
+    }
     classes.clear();
     dfree(doc_list);
     u32 present = 0;
     for (auto& v : by) present += !v.empty();
-    if (present <= 1) {
+    if (present <= 1 && identity) {
       for (u32 k = 0; k < 5; k++)
         if (!by[k].empty()) classes.push_back(RootClass{rc(k), INVALID, by[k].size(), k == 4});
       return 0;
@@ -842,6 +852,8 @@ struct crdt_engine {
     } else {
       HIPCHK(hipMemcpyAsync(segs, seg_h.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
       r = push_agent_counts();
+      if (r) return r;
+      r = plan_classes();  // (launch order: the new streams' lengths)
       if (r) return r;
     }
     if (n_docs) {
