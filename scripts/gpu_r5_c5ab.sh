@@ -1,4 +1,4 @@
-# Round 5: GPU tests of the product library, then an A/B of LIBS on config 5 (4,096 documents,
+# Round 5: GPU tests of the product library, then an A/B of LIBS on config 5 (C5DOCS documents,
 # prof_replay.py --config5) and automerge-paper (8,192), same box.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -10,7 +10,7 @@ if [ -z "$NOTESTS" ]; then
   [ $rc -le 1 ] || exit $rc
 fi
 for L in $LIBS; do
-  echo -n "c5 4096 $L "; CRDT_GPU_LIB=$B/$L timeout -k 10 300 python scripts/prof_replay.py --docs 4096 --config5 --clean | tail -1 || exit 1
+  echo -n "c5 ${C5DOCS:-8192} $L "; CRDT_GPU_LIB=$B/$L timeout -k 10 300 python scripts/prof_replay.py --docs ${C5DOCS:-8192} --config5 --clean | tail -1 || exit 1
 done
 for L in $LIBS; do
   echo -n "ap 8192 $L "; CRDT_GPU_LIB=$B/$L timeout -k 10 120 python scripts/prof_replay.py --docs 8192 --clean | tail -1 || exit 1

@@ -6,6 +6,14 @@
 static unsigned long long g_stat[128];
 #define CRDT_STAT(k, v) (g_stat[(k)] += (unsigned long long)(v))
 #define WCPU_COUNT(kind, f) (g_stat[124 + (kind > 3 ? 3 : kind)]++)  // (context reads / writes / cache reads / other)
+// memory lines (128 B) each op touches, by pool: WaveCPU reports the bytes its WaveGPU twin reads /
+// writes (WCPU_MEM); an epoch (one fast_txn / apply_txn call, CRDT_MEM_EPOCH) counts every line it
+// touched once, as a read line and / or a written line
+void emu_mem_touch(const void* p, unsigned long long n, int wr);
+void emu_mem_epoch();
+static const void* g_mem_doc = nullptr;  // (the EmuDoc being replayed)
+#define WCPU_MEM(p, n, wr) emu_mem_touch((const void*)(p), (unsigned long long)(n), (wr))
+#define CRDT_MEM_EPOCH() emu_mem_epoch()
 #endif
 #include <cstdio>
 #include <cstdlib>
@@ -146,6 +154,9 @@ struct EmuDoc {
   }
 
   template <int LL> int run_impl() {
+#ifdef CRDT_EMU_STATS
+    g_mem_doc = this;
+#endif
     bool first = true;
     while (true) {
       Pools p = pools();
@@ -183,7 +194,71 @@ struct EmuDoc {
 
 }  // namespace
 
+#ifdef CRDT_EMU_STATS
+#include <unordered_map>
+enum { MC_LEAVES, MC_DIR, MC_SOL, MC_LEAF_OF, MC_AGENT_OF, MC_LAG, MC_CWO, MC_ARUN, MC_DELS, MC_DD, MC_DDB, MC_TXNS,
+       MC_PARENTS, MC_FRONTIER, MC_AGENTS, MC_GROUPS, MC_RECS, MC_OTHER, MC_N };
+static std::unordered_map<unsigned long long, unsigned> g_mem_lines;
+static unsigned long long g_mem_rd[MC_N], g_mem_wr[MC_N], g_mem_epochs;
+template <class V> static bool in_vec(const V& v, const void* p) {
+  const char* a = (const char*)v.data();
+  return (const char*)p >= a && (const char*)p < a + v.size() * sizeof(v[0]);
+}
+static int mem_cat(const void* p) {
+  const EmuDoc* d = (const EmuDoc*)g_mem_doc;
+  if (!d) return MC_OTHER;
+  if (in_vec(d->leaves, p)) return MC_LEAVES;
+  if (in_vec(d->dir_leaf, p) || in_vec(d->dir_vis, p)) return MC_DIR;
+  if (in_vec(d->sol, p)) return MC_SOL;
+  if (in_vec(d->leaf_of, p)) return MC_LEAF_OF;
+  if (in_vec(d->agent_of, p)) return MC_AGENT_OF;
+  if (in_vec(d->leaf_agents, p)) return MC_LAG;
+  if (in_vec(d->cwo, p)) return MC_CWO;
+  if (in_vec(d->arun, p)) return MC_ARUN;
+  if (in_vec(d->dels, p)) return MC_DELS;
+  if (in_vec(d->dd, p)) return MC_DD;
+  if (in_vec(d->ddb, p)) return MC_DDB;
+  if (in_vec(d->txns, p)) return MC_TXNS;
+  if (in_vec(d->parents, p)) return MC_PARENTS;
+  if (in_vec(d->frontier, p)) return MC_FRONTIER;
+  if (in_vec(d->agent_tab, p)) return MC_AGENTS;
+  if (in_vec(d->groups, p)) return MC_GROUPS;
+  if (in_vec(d->recs, p)) return MC_RECS;
+  return MC_OTHER;
+}
+void emu_mem_touch(const void* p, unsigned long long n, int wr) {
+  if (!n) return;
+  unsigned long long a = (unsigned long long)p;
+  unsigned c = (unsigned)mem_cat(p);
+  for (unsigned long long ln = a >> 7; ln <= (a + n - 1) >> 7; ln++) {
+    unsigned& f = g_mem_lines[ln];
+    f |= (wr ? 2u : 1u) | ((c + 1u) << 2);
+  }
+}
+void emu_mem_epoch() {
+  for (auto& kv : g_mem_lines) {
+    unsigned c = (kv.second >> 2) - 1u;
+    if (c >= MC_N) c = MC_OTHER;
+    if (kv.second & 1u) g_mem_rd[c]++;
+    if (kv.second & 2u) g_mem_wr[c]++;
+  }
+  g_mem_lines.clear();
+  g_mem_epochs++;
+}
+#endif
+
 extern "C" {
+
+#ifdef CRDT_EMU_STATS
+// lines read / written per pool (MC_* order) summed over every epoch so far; returns the epochs
+unsigned long long emu_mem_stats(unsigned long long* rd, unsigned long long* wr, int reset) {
+  emu_mem_epoch();
+  for (int k = 0; k < MC_N; k++) { rd[k] = g_mem_rd[k]; wr[k] = g_mem_wr[k]; if (reset) g_mem_rd[k] = g_mem_wr[k] = 0; }
+  unsigned long long e = g_mem_epochs;
+  if (reset) g_mem_epochs = 0;
+  return e;
+}
+#endif
 
 void* emu_new(uint32_t leaf_cap) {
   if (leaf_cap != 4 && leaf_cap != 32) return nullptr;

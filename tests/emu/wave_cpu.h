@@ -15,6 +15,11 @@
 #ifndef WCPU_COUNT
 #define WCPU_COUNT(kind, f) ((void)0)
 #endif
+// (statistics build: the bytes each method reads / writes in device memory, as the WaveGPU method
+// accesses them -- a lane-parallel load touches every lane's element)
+#ifndef WCPU_MEM
+#define WCPU_MEM(p, n, wr) ((void)0)
+#endif
 
 namespace crdt {
 
@@ -37,43 +42,61 @@ struct WaveCPU {
   void x_store_state(DocState* p, u32 base) const { std::memcpy(p, x + base, sizeof(DocState)); }
 
   static u64 clock() { return 0; }
-  u32 ld(const u32* p) const { return *p; }
-  u32 ld_raw(const u32* p) const { return *p; }
-  void ld_raw2(const u32* p, u32& a, u32& b) const { a = p[0]; b = p[1]; }
+  u32 ld(const u32* p) const { WCPU_MEM(p, 4, 0); return *p; }
+  u32 ld_raw(const u32* p) const { WCPU_MEM(p, 4, 0); return *p; }
+  void ld_raw2(const u32* p, u32& a, u32& b) const { WCPU_MEM(p, 8, 0); a = p[0]; b = p[1]; }
   static u32 uni_(u32 x) { return x; }
-  void st(u32* p, u32 v) const { *p = v; }
-  void st(i32* p, i32 v) const { *p = v; }
-  void st_lanes(u32* p, u32 v, u32 n) const { if (n) *p = v; }
-  template <class T> T ldT(const T* p) const { return *p; }
-  template <class T> void stT(T* p, const T& v) const { *p = v; }
-  AgentRec ld_agent(const AgentRec* p) const { return *p; }
-  void st_agent_tail(AgentRec* p, u32 key, u32 order, u32 len) const { p->tkey = key; p->torder = order; p->tlen = len; }
-  ARun ld_arun(const ARun* p) const { return *p; }
-  void st_arun(ARun* p, const ARun& v) const { *p = v; }
-  CwoRun ld_cwo(const CwoRun* p) const { return *p; }
-  void st_cwo(CwoRun* p, const CwoRun& v) const { *p = v; }
-  DelRun ld_del(const DelRun* p) const { return *p; }
-  void st_del(DelRun* p, const DelRun& v) const { *p = v; }
-  DDRun ld_dd(const DDRun* p) const { return *p; }
-  void st_dd(DDRun* p, const DDRun& v) const { *p = v; }
-  TxnRec ld_txn(const TxnRec* p) const { return *p; }
-  void st_txn(TxnRec* p, const TxnRec& v) const { *p = v; }
-  Rec ld_rec(const Rec* p) const { return *p; }
+  void st(u32* p, u32 v) const { WCPU_MEM(p, 4, 1); *p = v; }
+  void st(i32* p, i32 v) const { WCPU_MEM(p, 4, 1); *p = v; }
+  void st_lanes(u32* p, u32 v, u32 n) const { if (n) { WCPU_MEM(p, 4, 1); *p = v; } }
+  template <class T> T ldT(const T* p) const { WCPU_MEM(p, sizeof(T), 0); return *p; }
+  template <class T> void stT(T* p, const T& v) const { WCPU_MEM(p, sizeof(T), 1); *p = v; }
+  AgentRec ld_agent(const AgentRec* p) const { WCPU_MEM(p, sizeof(AgentRec), 0); return *p; }
+  void st_agent_tail(AgentRec* p, u32 key, u32 order, u32 len) const { WCPU_MEM(&p->tkey, 12, 1); p->tkey = key; p->torder = order; p->tlen = len; }
+  ARun ld_arun(const ARun* p) const { WCPU_MEM(p, sizeof(ARun), 0); return *p; }
+  void st_arun(ARun* p, const ARun& v) const { WCPU_MEM(p, sizeof(ARun), 1); *p = v; }
+  CwoRun ld_cwo(const CwoRun* p) const { WCPU_MEM(p, sizeof(CwoRun), 0); return *p; }
+  void st_cwo(CwoRun* p, const CwoRun& v) const { WCPU_MEM(p, sizeof(CwoRun), 1); *p = v; }
+  DelRun ld_del(const DelRun* p) const { WCPU_MEM(p, sizeof(DelRun), 0); return *p; }
+  void st_del(DelRun* p, const DelRun& v) const { WCPU_MEM(p, sizeof(DelRun), 1); *p = v; }
+  DDRun ld_dd(const DDRun* p) const { WCPU_MEM(p, sizeof(DDRun), 0); return *p; }
+  void st_dd(DDRun* p, const DDRun& v) const { WCPU_MEM(p, sizeof(DDRun), 1); *p = v; }
+  TxnRec ld_txn(const TxnRec* p) const { WCPU_MEM(p, sizeof(TxnRec), 0); return *p; }
+  void st_txn(TxnRec* p, const TxnRec& v) const { WCPU_MEM(p, sizeof(TxnRec), 1); *p = v; }
+  Rec ld_rec(const Rec* p) const { WCPU_MEM(p, sizeof(Rec), 0); return *p; }
   template <u32 M = 1, class T> static T* at(T* base, u32 idx) { return base + (u64)idx * M; }
   void st_state(DocState* p, const DocState& s) const { *p = s; }
   DocState ld_state(const DocState* p) const { return *p; }
   DocSeg ld_seg(const DocSeg* p) const { return *p; }
-  void fill(u32* p, u32 n, u32 v) const { for (u32 k = 0; k < n; k++) p[k] = v; }
-  void fill16(u16* p, u32 n, u32 v) const { for (u32 k = 0; k < n; k++) p[k] = (u16)v; }
-  u32 ld16(const u16* p) const { return *p; }
-  void zero_leaf(Span* p, u32 n) const { std::memset(p, 0, sizeof(Span) * n); }
+  void fill(u32* p, u32 n, u32 v) const { WCPU_MEM(p, 4ull * n, 1); for (u32 k = 0; k < n; k++) p[k] = v; }
+  void fill16(u16* p, u32 n, u32 v) const { WCPU_MEM(p, 2ull * n, 1); for (u32 k = 0; k < n; k++) p[k] = (u16)v; }
+  u32 ld16(const u16* p) const { WCPU_MEM(p, 2, 0); return *p; }
+  void zero_leaf(Span* p, u32 n) const { WCPU_MEM(p, sizeof(Span) * n, 1); std::memset(p, 0, sizeof(Span) * n); }
 
   template <class T> static u32 rkey(const T& r) { return ((const u32*)&r)[0]; }
   static u32 rlen(const ARun& r) { return r.len; }
   static u32 rlen(const CwoRun& r) { return r.len; }
   static u32 rlen(const DDRun& r) { return r.len; }
   static u32 rlen(const TxnRec& r) { return r.len; }
+  // the elements the GPU's 64-ary search samples (wave_gpu.h search / search_first), key(i) of element i
+  template <class T, class K> void search_touch(const T* b, u32 n, u32 x, K key) const {
+    u32 lo = 0, hi = n;
+    while (hi - lo > 64) {
+      u32 step = (hi - lo + 63) / 64, best = INVALID;
+      for (u32 l = 0; l < 64; l++) {
+        u32 idx = lo + l * step;
+        if (idx >= hi) break;
+        WCPU_MEM(b + idx, sizeof(T), 0);
+        if (key(idx) <= x) best = l;
+      }
+      if (best == INVALID) return;
+      lo = lo + best * step;
+      hi = lo + step < hi ? lo + step : hi;
+    }
+    WCPU_MEM(b + lo, sizeof(T) * (hi - lo), 0);
+  }
   template <class T> i32 search(const T* b, u32 n, u32 x) const {  // simple_rle.rs:18-25
+    search_touch(b, n, x, [&](u32 i) { return rkey(b[i]); });
     u32 lo = 0, hi = n;
     while (lo < hi) {
       u32 mid = (lo + hi) / 2;
@@ -94,17 +117,44 @@ struct WaveCPU {
   DDBlk ld_ddblk(const DDBlk* p) const { return *p; }
   void st_ddblk(DDBlk* p, const DDBlk& v) const { *p = v; }
   i32 search_first(const DDBlk* b, u32 n, u32 x) const {
+    search_touch(b, n, x, [&](u32 i) { return b[i].first; });
     i32 r = -1;
     for (u32 i = 0; i < n; i++) if (b[i].first <= x) r = (i32)i;
     return r;
   }
-  u32 dd_count_le(const DDRun* blk, u32 cnt, u32 x) const { u32 k = 0; for (u32 i = 0; i < cnt; i++) k += blk[i].key <= x; return k; }
-  u32 dd_split(const DDRun* src, DDRun* dst) const { for (u32 i = 32; i < 64; i++) dst[i - 32] = src[i]; return dst[0].key; }
+  // the directory's top level (WaveGPU: in LDS): word j = the first key of block 64 j; every
+  // search checks it against the directory (a stale word aborts)
+  u32 dt[DDT_LDS] = {};
+  i32 dd_search_top(const DDBlk* b, u32 nb, u32 x) const {
+    u32 nt = (nb + 63u) >> 6;
+    for (u32 j = 0; j < nt; j++)
+      if (dt[j] != b[64u * j].first) {
+        std::fprintf(stderr, "wave_cpu: stale double-delete top level (word %u: %u, block %u)\n", j, dt[j], b[64u * j].first);
+        std::abort();
+      }
+    i32 g = -1;
+    for (u32 j = 0; j < nt; j++) if (dt[j] <= x) g = (i32)j;
+    if (g < 0) return -1;
+    u32 base = (u32)g * 64u, cnt = nb - base < 64u ? nb - base : 64u;
+    WCPU_MEM(b + base, sizeof(DDBlk) * cnt, 0);
+    i32 r = -1;
+    for (u32 i = 0; i < cnt; i++) if (b[base + i].first <= x) r = (i32)(base + i);
+    return r;
+  }
+  void ddt_set(u32 j, u32 key) { dt[j] = key; }
+  void ddt_rebuild(const DDBlk* b, u32 j0, u32 nb) {
+    u32 nt = (nb + 63u) >> 6;
+    for (u32 j = j0; j < nt; j++) { WCPU_MEM(b + 64u * j, sizeof(DDBlk), 0); dt[j] = b[64u * j].first; }
+  }
+  u32 dd_count_le(const DDRun* blk, u32 cnt, u32 x) const { WCPU_MEM(blk, sizeof(DDRun) * cnt, 0); u32 k = 0; for (u32 i = 0; i < cnt; i++) k += blk[i].key <= x; return k; }
+  u32 dd_split(const DDRun* src, DDRun* dst) const { WCPU_MEM(src + 32, sizeof(DDRun) * 32, 0); WCPU_MEM(dst, sizeof(DDRun) * 32, 1); for (u32 i = 32; i < 64; i++) dst[i - 32] = src[i]; return dst[0].key; }
   void dd_block_insert(DDRun* blk, u32 cnt, u32 i, const DDRun& r) const {
+    WCPU_MEM(blk, sizeof(DDRun) * cnt, 0); WCPU_MEM(blk + i, sizeof(DDRun) * (cnt + 1 - i), 1);
     for (u32 k = cnt; k > i; k--) blk[k] = blk[k - 1];
     blk[i] = r;
   }
   void ddb_insert(DDBlk* b, u32 n, u32 at, const DDBlk& v) const {
+    WCPU_MEM(b + at, sizeof(DDBlk) * (n - at), 0); WCPU_MEM(b + at, sizeof(DDBlk) * (n + 1 - at), 1);
     for (u32 k = n; k > at; k--) b[k] = b[k - 1];
     b[at] = v;
   }
@@ -112,12 +162,13 @@ struct WaveCPU {
 
   // leaf cache
   u32 cache_load(const Span* p) {
+    WCPU_MEM(p, sizeof(Span) * L, 0);
     u32 n = 0;
     for (u32 i = 0; i < 64; i++) c[i] = i < (u32)L ? p[i] : Span{0, 0, 0, 0};
     for (u32 i = 0; i < (u32)L; i++) n += c[i].len != 0;
     return n;
   }
-  void cache_store(Span* p) const { for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
+  void cache_store(Span* p) const { WCPU_MEM(p, sizeof(Span) * L, 1); for (u32 i = 0; i < (u32)L; i++) p[i] = c[i]; }
   Span cget(u32 i) const { WCPU_COUNT(2, 0); return c[i & 63]; }
   u32 cget_order(u32 i) const { WCPU_COUNT(3, 0); return c[i & 63].order; }
   i32 cget_len(u32 i) const { WCPU_COUNT(3, 1); return c[i & 63].len; }
@@ -125,17 +176,18 @@ struct WaveCPU {
   void cset_len(u32 i, i32 len) { c[i & 63].len = len; }
   template <class F> void cset_lanes(u32 a, u32 b, F f) { for (u32 l = a; l < b && l < 64; l++) c[l] = f(l); }
   template <class F> void leaf_write_lanes(Span* dst, u32 n, F f) const {
+    WCPU_MEM(dst, sizeof(Span) * L, 1);
     for (u32 l = 0; l < (u32)L; l++) dst[l] = l < n ? f(l) : Span{0, 0, 0, 0};
   }
   u32 cache_vis_from(u32 a) const { u32 t = 0; for (u32 i = a; i < 64; i++) t += clen(c[i]); return t; }
   void rank_load(const AgentRec*, u32) const {}
   u32 rank_of(const AgentRec* agents, u32, u32 a) const { return agents[a].rank; }
   mutable const u16* oag = nullptr;  // (scan_gather's map, read by scan_batch)
-  u32 scan_gather(u32, const u16* m) const { oag = m; return 0u; }
+  u32 scan_gather(u32 nn, const u16* m) const { for (u32 j = 0; j < nn && j < 64; j++) WCPU_MEM(m + c[j].order, 2, 0); oag = m; return 0u; }
   // agent rows: word 0 (valid) is what the replay sees; a current row must hold exactly the map's
   // agents of the cached leaf's entries (checked here: a stale row taken as current aborts)
   mutable const u32* lag_p = nullptr;
-  u32 lag_ld(const u32* p) const { lag_p = p; return p[0]; }
+  u32 lag_ld(const u32* p) const { WCPU_MEM(p, 4 * lag_words(L), 0); lag_p = p; return p[0]; }
   u32 lag_valid(u32 lw) const { return lw == 1u; }
   u32 lag_agents(u32, u32 n, const u16* m, u32 tkey, u32 tlen, u32 tagent) const {
     oag = m;
@@ -151,6 +203,7 @@ struct WaveCPU {
     return 0u;
   }
   void lag_store(u32* p, u32, u32 n, u32 tkey, u32 tlen, u32 tagent, u32, u32 n_agents, const AgentRec* agents) const {
+    WCPU_MEM(p, 4 * lag_words(L), 1);
     for (u32 j = 0; j < (u32)L / 2; j++) p[lag_words(L) / 2 + j] = 0;
     u32 mr = 0, omin = 0xFFFFFFFFu, omax = 0, mixed = n == 0 ? LAG_MIXED : 0u;
     for (u32 j = 0; j < n; j++) {
@@ -172,8 +225,10 @@ struct WaveCPU {
   // pass each with no event: origin_left X, rank below my_rank, first order not orr)
   u32 skip_scan(const u32* row, u32 a, u32 cnt, const u32* lag, u32 X, u32 orr, u32 my_rank, u32 n_agents,
                 const Span* leaves, const AgentRec* agents, u32& leaf) const {
+    WCPU_MEM(row, 4 * 64, 0);
     for (u32 j = a; j < cnt; j++) {
       const u32* q = lag + (size_t)row[j] * lag_words(L);
+      WCPU_MEM(q, 4 * (LAG_OMAX + 1), 0);
       bool skip = q[0] == 1u && q[1] == n_agents && q[LAG_OL] == X && q[LAG_RANK] < my_rank &&
                   orr - q[LAG_OMIN] > q[LAG_OMAX] - q[LAG_OMIN];
       if (!skip) { leaf = row[j]; return j; }
@@ -212,6 +267,7 @@ struct WaveCPU {
   u64 lanes_in(u32 a, u32 b) const { u64 m = 0; for (u32 i = a; i < b && i < 64; i++) m |= 1ull << i; return m; }
   static u32 first_lane(u64 m) { return (u32)__builtin_ctzll(m); }
   i32 peek_find_order(const Span* p, u32 order, u32& start) const {
+    WCPU_MEM(p, sizeof(Span) * L, 0);
     for (u32 i = 0; i < (u32)L; i++)
       if (p[i].len != 0 && order >= p[i].order && order - p[i].order < slen(p[i])) { start = p[i].order; return (i32)i; }
     return -1;
@@ -233,6 +289,7 @@ struct WaveCPU {
   }
   Span mv[64];
   void cache_write_moved(Span* dst, u32 idx, u32 n, u32 padding) {
+    WCPU_MEM(dst, sizeof(Span) * L, 1);
     for (u32 j = 0; j < 64; j++) {
       u32 src = j + idx - padding;
       mv[j] = (j < (u32)L && j >= padding && src < n) ? c[src] : Span{0, 0, 0, 0};
@@ -241,10 +298,10 @@ struct WaveCPU {
   }
   void cache_from_moved() { for (u32 j = 0; j < 64; j++) c[j] = mv[j]; }
   Span pfr[64];
-  void leaf_prefetch(const Span* p) { for (u32 j = 0; j < 64; j++) pfr[j] = j < (u32)L ? p[j] : Span{0, 0, 0, 0}; }
+  void leaf_prefetch(const Span* p) { WCPU_MEM(p, sizeof(Span) * L, 0); for (u32 j = 0; j < 64; j++) pfr[j] = j < (u32)L ? p[j] : Span{0, 0, 0, 0}; }
   u32 cache_from_prefetch() { u32 n = 0; for (u32 j = 0; j < 64; j++) { c[j] = pfr[j]; n += c[j].len != 0; } return n; }
   void fill_runs(u32* base, u32 a, u32 b, u32 v) const {
-    for (u32 i = a; i < b; i++) for (u32 t = 0; t < slen(c[i]); t++) base[c[i].order + t] = v;
+    for (u32 i = a; i < b; i++) { WCPU_MEM(base + c[i].order, 4ull * slen(c[i]), 1); for (u32 t = 0; t < slen(c[i]); t++) base[c[i].order + t] = v; }
   }
   void cache_clear(u32 a, u32 b) { for (u32 i = a; i < b; i++) c[i] = Span{0, 0, 0, 0}; }
   void cache_shift_right(u32 idx, u32 n, u32 k) {
@@ -253,10 +310,12 @@ struct WaveCPU {
   }
   Rec rb[64], qb[64];
   void rec_load2(const Rec* p, u32 n, u32 n_ahead) {
+    WCPU_MEM(p, sizeof(Rec) * n, 0); WCPU_MEM(p + 64, sizeof(Rec) * n_ahead, 0);
     for (u32 i = 0; i < n; i++) rb[i] = p[i];
     for (u32 i = 0; i < n_ahead; i++) qb[i] = p[64 + i];
   }
   void rec_slide(u32 d, const Rec* p_ahead, u32 n_ahead) {
+    WCPU_MEM(p_ahead, sizeof(Rec) * n_ahead, 0);
     Rec t[128];
     for (u32 i = 0; i < 64; i++) { t[i] = rb[i]; t[64 + i] = qb[i]; }
     for (u32 i = 0; i < 64; i++) rb[i] = t[(i + d) & 127];
@@ -268,12 +327,14 @@ struct WaveCPU {
   }
   // the GPU backend's scans over 64 records at p (no window move); len0 = the first txn's length
   u32 typing_scan_at(const Rec* p, u32 nv, u32 remote, u32 compact, u32 agent, u32 ow1, u32 ow3, u32& total, u32& len0) const {
+    WCPU_MEM(p, sizeof(Rec) * nv, 0);
     Rec t[64];
     for (u32 i = 0; i < nv; i++) t[i] = p[i];
     len0 = (compact & remote) ? rc_len(t[0]) : t[0].w3;
     return typing_scan_b(t, 0u, nv, remote, compact, agent, ow1, ow3, total);
   }
   u32 delete_scan_at(const Rec* p, u32 nv, u32 remote, u32 compact, u32 agent, u32 delta) const {
+    WCPU_MEM(p, sizeof(Rec) * nv, 0);
     Rec t[64];
     for (u32 i = 0; i < nv; i++) t[i] = p[i];
     return delete_scan_b(t, 0u, nv, remote, compact, agent, delta);
@@ -286,6 +347,7 @@ struct WaveCPU {
   }
   u32 frontier_advance(u32* f, u32 nfr, u32 f0, const u32* pp, u32 np, u32 p0, u32 first, u32 last, u32 cap,
                        u32& nf0) const {
+    WCPU_MEM(f, 4ull * nfr + 4, 0); WCPU_MEM(pp, 4ull * np, 0); WCPU_MEM(f, 4ull * nfr + 4, 1);
     std::vector<u32> h(nfr);
     for (u32 k = 0; k < nfr; k++) h[k] = k == 0 ? f0 : f[k];
     for (u32 k = 0; k < nfr; k++) if (h[k] == first) return 0u;
@@ -391,6 +453,7 @@ struct WaveCPU {
     return n;
   }
   void st_del_run(DelRun* p, u32 cnt, u32 key0, u32 t0) const {
+    WCPU_MEM(p, sizeof(DelRun) * cnt, 1);
     for (u32 j = 0; j < cnt; j++) p[j] = DelRun{key0 + j, t0 - j, 1u};
   }
 
@@ -426,17 +489,19 @@ struct WaveCPU {
     return false;
   }
   u32 root_vis_before(u32 g) const { u32 t = 0; for (u32 i = 0; i < g; i++) t += gv[i]; return t; }
-  u32 blk_vis_before(const u32* dv, u32 i) const { u32 t = 0; for (u32 k = 0; k < i; k++) t += dv[k]; return t; }
+  u32 blk_vis_before(const u32* dv, u32 i) const { WCPU_MEM(dv, 4 * 64, 0); u32 t = 0; for (u32 k = 0; k < i; k++) t += dv[k]; return t; }
   u32 cache_vis_before(u32 idx) const { u32 t = 0; for (u32 i = 0; i < idx; i++) t += clen(c[i]); return t; }
   u32 peek_vis_before(const Span* p, u32 idx, i32& len_idx) const {
+    WCPU_MEM(p, sizeof(Span) * L, 0);
     u32 t = 0;
     for (u32 i = 0; i < idx; i++) t += clen(p[i]);
     len_idx = p[idx].len;
     return t;
   }
-  void st_span(Span* p, const Span& s) const { *p = s; }
+  void st_span(Span* p, const Span& s) const { WCPU_MEM(p, sizeof(Span), 1); *p = s; }
   void st_probe(uint4* p, u32 a, u32 s, u32 ps, u32 dl) const { *p = make_uint4(a, s, ps, dl); }
   bool blk_find_pos(const u32* dv, const u32* dl, u32 cnt, u32 rem, u32& i, u32& before, u32& leaf) const {
+    WCPU_MEM(dv, 4 * 64, 0); WCPU_MEM(dl, 4 * 64, 0);
     u32 acc = 0;
     for (u32 k = 0; k < cnt; k++) {
       if (rem < acc + dv[k]) { i = k; before = acc; leaf = dl[k]; return true; }
@@ -447,7 +512,7 @@ struct WaveCPU {
   // (the GPU's row_ld returns a row one slot per lane; here a digest of the row, which blk_insert
   // checks against the row's current contents: the early-requested rows must still be current)
   static u32 row_digest(const u32* p) { u32 h = 2166136261u; for (u32 k = 0; k < 64; k++) h = (h ^ p[k]) * 16777619u; return h; }
-  u32 row_ld(const u32* p) const { return row_digest(p); }
+  u32 row_ld(const u32* p) const { WCPU_MEM(p, 4 * 64, 0); return row_digest(p); }
   static void row_check(u32 ol, u32 ov, const u32* dl, const u32* dv) {
     if (ol != row_digest(dl) || ov != row_digest(dv)) {
       std::fprintf(stderr, "wave_cpu: directory row changed between row_ld and its use\n");
@@ -456,6 +521,8 @@ struct WaveCPU {
   }
   void blk_insert_at(u32 ol, u32 ov, u32* dl, u32* dv, u32 cnt, u32 i, u32 vis_i, u32 leaf, u32 vis, u32* sol, u32 blk) const {
     row_check(ol, ov, dl, dv);
+    WCPU_MEM(dl, 4 * 64, 1); WCPU_MEM(dv, 4 * 64, 1);
+    for (u32 k = i + 1; k <= cnt; k++) WCPU_MEM(sol + 2 * (k == i + 1 ? leaf : dl[k - 1]), 4, 1);
     dv[i] = vis_i;
     for (u32 k = cnt; k > i + 1; k--) { dl[k] = dl[k - 1]; dv[k] = dv[k - 1]; }
     dl[i + 1] = leaf;
@@ -464,6 +531,8 @@ struct WaveCPU {
   }
   u32 blk_split_r(u32 rl, u32 rv, const u32* dl, const u32* dv, u32* ndl, u32* ndv, u32* sol, u32 nb) const {
     row_check(rl, rv, dl, dv);
+    WCPU_MEM(ndl, 4 * 32, 1); WCPU_MEM(ndv, 4 * 32, 1);
+    for (u32 k = 32; k < 64; k++) WCPU_MEM(sol + 2 * dl[k], 4, 1);
     u32 t = 0;
     for (u32 k = 32; k < 64; k++) {
       ndl[k - 32] = dl[k];

@@ -24,6 +24,9 @@ typedef int64_t i64;
 #define CRDT_HD __host__ __device__ __forceinline__
 // Event counters of the CPU emulation's statistics build (tests/emu stats: path counts for the
 // design notes); nothing in the product builds.
+#ifndef CRDT_MEM_EPOCH  // (emulator statistics build: one op's memory lines end here)
+#define CRDT_MEM_EPOCH() ((void)0)
+#endif
 #ifndef CRDT_STAT
 #define CRDT_STAT(k, v) ((void)0)
 #endif
@@ -48,11 +51,12 @@ constexpr u32 GROUP = 64;                 // directory slots per block (one wave
 // CU's LDS, so a document can have up to ROOT_CAP_MAX blocks = at least 32*(ROOT_CAP_MAX-1)
 // leaves (every block but the first holds >= 32 slots) = 13.9M entries at the release layout.
 constexpr u32 ROOT_CAP_MIN = 256;
-// (the two-level root's top entries: 12 B each + two words + the agent ranks + the prefetch row
-// within 160 KiB, floor((163840 - 8 - 4 * RANK_LDS - 4 * PF_LDS) / 12 / 64) * 64; static_assert below)
+// (the two-level root's top entries: 12 B each + two words + the agent ranks + the prefetch row +
+// the double-delete top level within 160 KiB, floor((163840 - 8 - 4 * (RANK_LDS + PF_LDS + DDT_LDS))
+// / 12 / 64) * 64; static_assert below)
 constexpr u32 ROOT_CAP_MAX = 13568;
 // The flat LDS root also keeps a block -> group map (4 B per group: 16 B per group in all), so its
-// largest class is floor((163840 - 4 * RANK_LDS - 4 * PF_LDS) / 16 / 64) * 64 groups; documents past it use
+// largest class is floor((163840 - 4 * (RANK_LDS + PF_LDS + DDT_LDS)) / 16 / 64) * 64 groups; documents past it use
 // the two-level root.
 constexpr u32 ROOT_CAP_LDS = 10176;
 // Agent ranks (the integrate tie-break's name order, doc.rs:207) of documents with at most
@@ -63,9 +67,15 @@ constexpr u32 RANK_LDS = 64;
 // successor leaf into (LDS-DMA), the root (flat: blk / cnt / vis / block -> group map, 4 u32 per
 // group; two-level: 3 u32 per top entry + 2 words) and the agent ranks; 16 B aligned.
 constexpr u32 PF_LDS = 128;
+// The double-delete directory's top level (replay_core.h dd_upper): word j = the first key of
+// block 64 j, for documents with at most 64 * DDT_LDS blocks (others search the directory in HBM).
+// (32 words: the smallest root class's 4-wave workgroup stays within 1/8 of the CU's LDS, so
+// 8 waves per SIMD stay resident)
+constexpr u32 DDT_LDS = 32;
 CRDT_HD constexpr u32 wave_lds_words(u32 rcap, bool hr) {
-  return (PF_LDS + (hr ? 3u * rcap + 2u : 4u * rcap) + RANK_LDS + 3u) & ~3u;
+  return (PF_LDS + (hr ? 3u * rcap + 2u : 4u * rcap) + RANK_LDS + DDT_LDS + 3u) & ~3u;
 }
+static_assert(8u * 4u * 4u * wave_lds_words(ROOT_CAP_MIN, false) <= 163840u, "smallest root class: 8 waves per SIMD fit the LDS");
 static_assert(4u * wave_lds_words(ROOT_CAP_MAX, true) <= 163840u, "two-level root: one wave's LDS fits 160 KiB");
 static_assert(4u * wave_lds_words(ROOT_CAP_LDS, false) <= 163840u, "flat root: one wave's LDS fits 160 KiB");
 // Past it the root has two levels (wave_gpu.h HR): LDS top entries of rows that hold 32..64 groups

@@ -279,6 +279,8 @@ struct Replayer {
       p(T_TX_ORDER, t.order); p(T_TX_LEN, t.len); p(T_TX_SHADOW, t.shadow);
     }
     p(T_FR0, w.ld(fr()));
+    n = g(S_N_DDB);
+    if (n <= 64u * DDT_LDS) w.ddt_rebuild(ddb(), 0u, n);
   }
   // write-back tails -> HBM (the tables' last entries; frontier[0])
   // the tails a run of fast commits left behind next_order (F_BASE)
@@ -1041,7 +1043,7 @@ struct Replayer {
   // the position after the last entry with key <= x (entries are sorted by key)
   CRDT_HD DDPos dd_upper(u32 x) const {
     u32 nb = dd_nb();
-    i32 lb = nb ? w.search_first(ddb(), nb, x) : -1;
+    i32 lb = nb == 0u ? -1 : nb <= 64u * DDT_LDS ? w.dd_search_top(ddb(), nb, x) : w.search_first(ddb(), nb, x);
     if (lb < 0) return DDPos{0u, 0u};
     DDBlk B = w.ld_ddblk(ddb() + lb);
     u32 k = w.dd_count_le(dd() + (u64)B.phys * DD_BLK, B.cnt, x);  // >= 1: first <= x
@@ -1055,6 +1057,7 @@ struct Replayer {
       if (g(K_DD) == 0) return false;
       w.st_dd(dd(), r);
       w.st_ddblk(ddb(), DDBlk{0u, r.key, 1u, 0u});
+      w.ddt_set(0u, r.key);
       p(S_N_DDB, 1u);
       inc(S_N_DD);
       q = DDPos{0u, 0u};
@@ -1068,6 +1071,7 @@ struct Replayer {
       u32 np = nb;  // physical blocks are allocated in order
       u32 first2 = w.dd_split(dd() + (u64)bp * DD_BLK, dd() + (u64)np * DD_BLK);
       w.ddb_insert(ddb(), nb, q.lb + 1u, DDBlk{np, first2, DD_BLK / 2u, 0u});
+      if (nb + 1u <= 64u * DDT_LDS) w.ddt_rebuild(ddb(), (q.lb + 64u) >> 6, nb + 1u);  // (blocks 64 j >= q.lb + 1 moved)
       w.st(&ddb()[q.lb].cnt, DD_BLK / 2u);
       p(S_N_DDB, nb + 1u);
       if (q.i > DD_BLK / 2u) { q.lb += 1u; q.i -= DD_BLK / 2u; bp = np; }
@@ -1075,7 +1079,10 @@ struct Replayer {
     }
     w.dd_block_insert(dd() + (u64)bp * DD_BLK, bc, q.i, r);
     w.st(&ddb()[q.lb].cnt, bc + 1u);
-    if (q.i == 0u) w.st(&ddb()[q.lb].first, r.key);
+    if (q.i == 0u) {
+      w.st(&ddb()[q.lb].first, r.key);
+      if (((q.lb & 63u) == 0u) & ((q.lb >> 6) < DDT_LDS)) w.ddt_set(q.lb >> 6, r.key);
+    }
     inc(S_N_DD);
     return true;
   }
@@ -1264,7 +1271,7 @@ struct Replayer {
   // inl: the txn's single op (and for a remote txn its single parent) are gop / gpar, not records
   // after the header (a compact record, or a generated op)
   CRDT_HD i32 apply_txn(const Rec& h, u32 pos, bool remote, u32 inl, const Rec& gop, const Rec& gpar) {
-    CRDT_STAT(47, 1);
+    CRDT_STAT(47, 1); CRDT_MEM_EPOCH();
 #ifdef CRDT_PROF
     u64 prof_t0 = w.clock();
 #endif
@@ -2272,6 +2279,7 @@ struct Replayer {
   // gen: a txn expanded from a GEN record (header gh, op go; no record window, no runs).
   // kind: the record kind at `pos` (RTXN / LTXN / RC / LC; LTXN for a generated op).
   CRDT_HD u32 fast_txn(u32 pos, u32 kind, u32 gen, const Rec& gh, const Rec& go) {
+    CRDT_MEM_EPOCH();
     // set membership by bitmask: no lane-mask booleans
     cpt = ((1u << REC_RC | 1u << REC_LC) >> kind) & 1u;
     u32 remote = ((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u;

@@ -321,6 +321,32 @@ struct WaveGPU {
     u64 m = ballot(idx < hi && key <= x);
     return m ? (i32)(lo + (63 - __builtin_clzll(m))) : -1;
   }
+  // The directory's top level in LDS (crdt_types.h DDT_LDS; after the agent ranks): word j = the
+  // first key of block 64 j.  Last block with first key <= x, or -1, for nb <= 64 * DDT_LDS blocks:
+  // the top level picks the 64-block group (one LDS read), one read of the group's 64 records
+  // picks the block -- instead of the strided 64-ary search, whose first step reads 64 records
+  // 16 B wide in 64 different lines
+  __device__ __forceinline__ i32 dd_search_top(const DDBlk* b, u32 nb, u32 x) const {
+    u32 l = lane();
+    u32 nt = (nb + 63u) >> 6;
+    u32 key = l < nt ? (u32)rk[RANK_LDS + l] : 0u;
+    u64 m = ballot(l < nt && key <= x);
+    if (m == 0) return -1;
+    u32 base = (63u - (u32)__builtin_clzll(m)) << 6;
+    u32 cnt = nb - base < 64u ? nb - base : 64u;
+    u32 k2 = b[base + (l < cnt ? l : 0u)].first;
+    u64 m2 = ballot(l < cnt && k2 <= x);  // (bit 0: the group's first key is the top level's)
+    return (i32)(base + (63u - (u32)__builtin_clzll(m2)));
+  }
+  __device__ __forceinline__ void ddt_set(u32 j, u32 key) const {
+    if (lane() == 0u) rk[RANK_LDS + j] = key;
+  }
+  // top-level words [j0, ceil(nb / 64)) from the directory (after a block insert shifted it)
+  __device__ __forceinline__ void ddt_rebuild(const DDBlk* b, u32 j0, u32 nb) const {
+    u32 l = lane();
+    u32 nt = (nb + 63u) >> 6;
+    if (l >= j0 && l < nt) rk[RANK_LDS + l] = b[(u64)l << 6].first;
+  }
   // entries of one block (cnt >= 1) with key <= x
   __device__ __forceinline__ u32 dd_count_le(const DDRun* blk, u32 cnt, u32 x) const {
     u32 l = lane();
