@@ -5,7 +5,8 @@
 #ifdef CRDT_EMU_STATS  // statistics build (make stats): event counters of replay_core.h's CRDT_STAT sites
 static unsigned long long g_stat[128];
 #define CRDT_STAT(k, v) (g_stat[(k)] += (unsigned long long)(v))
-#define WCPU_COUNT(kind, f) (g_stat[124 + (kind > 3 ? 3 : kind)]++)  // (context reads / writes / cache reads / other)
+static unsigned long long g_field[2][192];  // context reads / writes per slot
+#define WCPU_COUNT(kind, f) (g_stat[124 + (kind > 3 ? 3 : kind)]++, (kind) < 2 ? (void)g_field[(kind)][(f) % 192]++ : (void)0)  // (context reads / writes / cache reads / other)
 // memory lines (128 B) each op touches, by pool: WaveCPU reports the bytes its WaveGPU twin reads /
 // writes (WCPU_MEM); an epoch (one fast_txn / apply_txn call, CRDT_MEM_EPOCH) counts every line it
 // touched once, as a read line and / or a written line
@@ -268,6 +269,9 @@ void* emu_new(uint32_t leaf_cap) {
 }
 void emu_free(void* h) { delete (EmuDoc*)h; }
 #ifdef CRDT_EMU_STATS
+void emu_field_stats(uint64_t* out, int reset) {  // [2][192]: context reads, then writes, per slot
+  for (int k = 0; k < 2 * 192; k++) { out[k] = g_field[k / 192][k % 192]; if (reset) g_field[k / 192][k % 192] = 0; }
+}
 void emu_stats(uint64_t* out, int reset) {
   for (int k = 0; k < 128; k++) { out[k] = g_stat[k]; if (reset) g_stat[k] = 0; }
 }
