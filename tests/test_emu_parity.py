@@ -1,5 +1,7 @@
 """CPU-only: the product's replay core (replay_core.h), run through the test-only CPU emulation
 backend, must reproduce the oracle exactly (entry layout included)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -161,3 +163,32 @@ def test_config1_probes(name, L):
         bad = np.argwhere((eans != oans).any(1))
         assert bad.size == 0, (int(bad[0][0]), eans[bad[0][0]], oans[bad[0][0]])
         assert (oans[:, 3] != 2).any() and (oans[:, 3] == 2).any()
+
+
+def test_config5_dd_top_level_threshold():
+    # the double-delete directory's LDS top level covers 64 * DDT_LDS blocks; a document past that
+    # searches the directory in HBM.  The emulator built with a one-word top level (64 blocks,
+    # tests/emu/build/libemu_ddt1.so) replays a config-5 history whose directory crosses it
+    # mid-replay: every top-level search is checked against the directory, and the state equals the
+    # oracle's.
+    import subprocess
+    import sys
+    import emu_lib
+    emu_lib.build()
+    code = (
+        "import sys; sys.path[:0] = ['tests', 'text-crdt-rust_amd']\n"
+        "from emu_lib import EmuDoc, diff_states\n"
+        "from oracle_lib import OracleDoc\n"
+        "from fuzz_gen import config5_wire\n"
+        "w = config5_wire(3, base_len=1 << 16, n_agents=16, rounds=24, ops=32)\n"
+        "o = OracleDoc(32, 16)\n"
+        "assert o.apply_remote_wire(w) == 0\n"
+        "e = EmuDoc(32)\n"
+        "assert e.run_wire(w, 48) == 0\n"
+        "assert e.check() == ''\n"
+        "assert diff_states(o.export(), e.export()) == []\n"
+        "print(o.sizes()['dd'])\n")
+    env = dict(os.environ, CRDT_EMU_LIB=os.path.join(emu_lib.EMU_DIR, "build", "libemu_ddt1.so"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=emu_lib.ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert int(r.stdout.split()[-1]) > 64 * 64  # (more double-delete entries than 64 full blocks hold)

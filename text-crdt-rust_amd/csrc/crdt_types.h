@@ -71,7 +71,10 @@ constexpr u32 PF_LDS = 128;
 // block 64 j, for documents with at most 64 * DDT_LDS blocks (others search the directory in HBM).
 // (32 words: the smallest root class's 4-wave workgroup stays within 1/8 of the CU's LDS, so
 // 8 waves per SIMD stay resident)
-constexpr u32 DDT_LDS = 32;
+#ifndef CRDT_DDT_LDS
+#define CRDT_DDT_LDS 32  // (the emulator's test build shrinks it to cross the threshold: tests/emu Makefile ddt)
+#endif
+constexpr u32 DDT_LDS = CRDT_DDT_LDS;
 CRDT_HD constexpr u32 wave_lds_words(u32 rcap, bool hr) {
   return (PF_LDS + (hr ? 3u * rcap + 2u : 4u * rcap) + RANK_LDS + DDT_LDS + 3u) & ~3u;
 }
