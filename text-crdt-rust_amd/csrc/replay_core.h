@@ -2275,6 +2275,46 @@ struct Replayer {
     fast_txn_commit(first, l);
     return 1;
   }
+  // A local delete of l visible items at pos that leaf_delete_span could not place in the cached
+  // leaf (it runs past the leaf's end, or the leaf has no room): local_deactivate's pieces one at a
+  // time (mutations.rs:520-570).  Each step finds the first visible item still at pos (the deleted
+  // ones are no longer visible there), deactivates its entry in place when the piece is the whole
+  // entry (mutate_entry, mutations.rs:265-273), else splits it the way mutate_entry +
+  // insert_internal do (delete_general: the deleted piece and the visible rest placed after the
+  // head, prepended onto the next entry of the same leaf when it can take them, the leaf split when
+  // they do not fit), and logs the piece (doc.rs:414-426, document order).  Only the first and the
+  // last piece split an entry, so at most two leaf splits: with the general path's room for one op
+  // (two free leaves) and delete-log room for l runs nothing can stop it part-way.  Returns 0,
+  // having changed nothing, when that room is not there or the range is past the document's end
+  // (the general path then reports it).
+  CRDT_HD u32 local_delete_pieces(u32 pos, u32 l, u32 first) {
+    if ((u64)pos + l > cur_len()) return 0;
+    if (g(K_LEAF) - g(S_N_LEAVES) < 2u) return 0;
+    if (g(K_DEL) - g(S_N_DEL) < l) return 0;
+    if (g(K_MAP) - first < l) return 0;
+    u32 key = first, rem = l;
+    while (rem) {
+      Cursor c;
+      bool ok = cursor_at_content_pos(pos, c);
+      CRDT_EXPECT(ok && c.idx < g(C_N) && w.cget_len(c.idx) > 0);
+      (void)ok;
+      u32 el = (u32)w.cget_len(c.idx);
+      u32 piece = el - c.off < rem ? el - c.off : rem;
+      u32 t = w.cget_order(c.idx) + c.off;
+      if ((c.off == 0u) & (piece == el)) {
+        w.cset_len(c.idx, -(i32)el);
+        p(C_NOW, g(C_NOW) - el);
+        p(C_DIRTY, 1u);
+      } else {
+        delete_general(c.idx, c.off, piece, 0u);
+      }
+      append_delete(key, t, piece);
+      key += piece;
+      rem -= piece;
+    }
+    fast_txn_commit(first, l);
+    return 1;
+  }
   // Returns the records consumed by a fast-path txn at `pos`, or 0 (use apply_txn).
   // gen: a txn expanded from a GEN record (header gh, op go; no record window, no runs).
   // kind: the record kind at `pos` (RTXN / LTXN / RC / LC; LTXN for a generated op).
@@ -2392,7 +2432,10 @@ struct Replayer {
           // a delete that runs past its first entry (local_deactivate over several entries of
           // the cached leaf): the multi-entry form, when it stays in the leaf
           i32 el = w.cget_len(c.idx);
-          if (el > 0 && c.off + l > (u32)el) return leaf_delete_span(c.idx, c.off, l, lp - g(C_VSTART), first) ? per : 0u;
+          if (el > 0 && c.off + l > (u32)el) {
+            if (leaf_delete_span(c.idx, c.off, l, lp - g(C_VSTART), first)) return per;
+            return local_delete_pieces(lp, l, first) ? per : 0u;  // (past the leaf, or no room in it)
+          }
         }
       }
     }
