@@ -606,10 +606,16 @@ struct crdt_engine {
     // their slots until its last one ends, so workgroups of similar documents, longest first, leave
     // the short ones to fill the end of the launch (mixed corpora: config 3).  Equal streams keep
     // the document order (stable sort).
+    // Documents of equal length that replay one shared record stream (the same history) go next
+    // to each other: a workgroup of equal histories ends together (config 5's 8 histories differ in
+    // cost at equal op counts).  Unshared streams sit at increasing offsets: document order.
     auto work = [&](u32 d) { return docs[d].staged.n_ops + docs[d].staged.n_txn; };
     bool identity = true;
     for (auto& v : by) {
-      std::stable_sort(v.begin(), v.end(), [&](u32 a, u32 b) { return work(a) > work(b); });
+      std::stable_sort(v.begin(), v.end(), [&](u32 a, u32 b) {
+        u64 wa = work(a), wb = work(b);
+        return wa != wb ? wa > wb : seg_h[a].rec_base < seg_h[b].rec_base;
+      });
       for (size_t i = 1; i < v.size(); i++) identity &= v[i] == v[i - 1] + 1u;
     }
     classes.clear();
