@@ -192,3 +192,26 @@ def test_config5_dd_top_level_threshold():
     r = subprocess.run([sys.executable, "-c", code], cwd=emu_lib.ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert int(r.stdout.split()[-1]) > 64 * 64  # (more double-delete entries than 64 full blocks hold)
+
+
+@pytest.mark.parametrize("L", [32, 4])
+def test_local_txn_parts(L):
+    # replace ops and multi-op local txns are encoded as single-op parts (host_plan.h
+    # encode_local_txn): same state as the oracle's one txn, an empty op skipped, and a txn of only
+    # empty ops keeps its empty-txn status
+    cases = [
+        ([1, 2, 1, 3], [[0, 0, 5], [2, 1, 0], [1, 0, 2], [0, 2, 1], [1, 0, 0], [3, 1, 2], [0, 0, 0]]),
+        ([2, 1], [[0, 0, 4], [1, 2, 3], [2, 1, 1]]),
+        ([1, 1], [[0, 0, 3], [0, 0, 0]]),
+    ]
+    for counts, patches in cases:
+        c = np.array(counts, np.uint32)
+        p = np.array(patches, np.uint32)
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        so = o.apply_trace(o.agent("x"), c, p)
+        e = EmuDoc(L)
+        se = e.run_local(e.agent("x"), c, p, 48 if L == 32 else 4)
+        assert se == so
+        if so == 0:
+            assert e.check() == ""
+            assert diff_states(o.export(), e.export()) == []

@@ -404,3 +404,25 @@ def test_same_wire_staged_once_and_fit_keeps_exact_maps():
             assert (e.digests() == np.uint64(o.digest())).all()
         assert_same(e.export(5), o.export())
         check_queries(e, 5, o)
+
+
+def test_local_txn_parts():
+    # replace ops and multi-op local txns replay as single-op parts on the fast paths: digests and
+    # exports equal the oracle's one txn; a txn of only empty ops keeps its empty-txn status
+    cases = [
+        ([1, 2, 1, 3], [[0, 0, 5], [2, 1, 0], [1, 0, 2], [0, 2, 1], [1, 0, 0], [3, 1, 2], [0, 0, 0]]),
+        ([2, 1], [[0, 0, 4], [1, 2, 3], [2, 1, 1]]),
+        ([1, 1], [[0, 0, 3], [0, 0, 0]]),
+    ]
+    for counts, patches in cases:
+        c = np.array(counts, np.uint32)
+        p = np.array(patches, np.uint32)
+        o = OracleDoc()
+        so = o.apply_trace(o.agent("x"), c, p)
+        e = crdt_amd.Engine(1, 32)
+        ag = e.agent_intern([0], ["x"])
+        st = e.apply_trace([0], int(ag[0]), c, p)
+        assert int(st[0]) == so
+        if so == 0:
+            assert int(e.digests()[0]) == o.digest()
+            assert_same(e.export(0), o.export())
