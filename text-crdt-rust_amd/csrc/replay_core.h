@@ -2297,8 +2297,12 @@ struct Replayer {
       Cursor c;
       bool ok = cursor_at_content_pos(pos, c);
       CRDT_EXPECT(ok && c.idx < g(C_N) && w.cget_len(c.idx) > 0);
-      (void)ok;
-      u32 el = (u32)w.cget_len(c.idx);
+      i32 sl = ok ? w.cget_len(c.idx) : 0;
+      if (sl <= (i32)c.off) {  // (cannot happen: pos + rem <= len holds at every step; never loop on it)
+        p(S_STATUS, (u32)ST_INTERNAL);
+        return 1;
+      }
+      u32 el = (u32)sl;
       u32 piece = el - c.off < rem ? el - c.off : rem;
       u32 t = w.cget_order(c.idx) + c.off;
       if ((c.off == 0u) & (piece == el)) {
