@@ -18,7 +18,12 @@ _lib = None
 
 
 def build() -> None:
-    subprocess.run(["make", "-s", "-C", EMU_DIR], check=True)
+    # (one make at a time: parallel test workers must not load a library another one is writing)
+    import fcntl
+    os.makedirs(os.path.join(EMU_DIR, "build"), exist_ok=True)
+    with open(os.path.join(EMU_DIR, "build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", EMU_DIR], check=True)
 
 
 def lib():
