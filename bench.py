@@ -16,6 +16,12 @@ batches of up to `--batch-docs` documents on one engine (8 batches at N = 1).  O
 corpus: per batch, the generator seeds of its documents are set on the device, then reset +
 replay + publish, and the digests are copied out on the device.  `value` = corpus ops / step time.
 
+The default line carries that corpus too: after the config-2 leg (and its engine is freed) the
+same config-4 leg runs (`--corpus-steps` timed passes after `--corpus-warmup` untimed ones) and is
+reported as the line's `corpus` object, with its own roofline, CPU baseline, parity and collective
+check, so `bench.py --gpus N` measures the north star's 1 M-document corpus (strong scaling over N)
+without a flag.  `--dist` initialises the RCCL process group even at world size 1.
+
 Multi-GPU: one process per GPU.  `--gpus N` with N > 1 started by hand spawns the N
 ranks through torch.distributed.run (the parent never touches a GPU); under torchrun the ranks
 read RANK / LOCAL_RANK / WORLD_SIZE.  The global corpus is N x `--docs` documents, sharded into
@@ -449,11 +455,16 @@ def oracle_digests_random(args, ids, threads: int):
         return np.array(list(ex.map(one, ids)), np.uint64)
 
 
-def run_config4(args, world: int, rank: int, gpu: int, dist):
+def run_config4(args, world: int, rank: int, gpu: int, dist, steps: int = None, warmup: int = None, cpu_s: float = None):
     """BASELINE config 4: the corpus sharded over ranks, each rank's share replayed
-    in resident batches on one engine.  Prints the bench line on rank 0."""
+    in resident batches on one engine.  Returns the line (rank 0; None elsewhere): the bench line of
+    `--workload config4`, and the `corpus` object of the default line (steps / warmup / CPU sample
+    given by the caller)."""
     import ctypes as C
     import torch
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    cpu_s = args.cpu_seconds if cpu_s is None else cpu_s
     D = args.corpus_docs
     lo, n = shard_balanced(np.ones(D), world, rank)
     B, batches = config4_batches(lo, n, args.batch_docs)
@@ -469,7 +480,7 @@ def run_config4(args, world: int, rank: int, gpu: int, dist):
                               "shards": [list(shard_balanced(np.ones(D), world, r)) for r in range(world)],
                               "batches_per_rank": len(batches),
                               "parity_ok": bool(all_dg.shape[0] == D and (all_dg == want).all()), "value": None}))
-        return
+        return None
     import crdt_amd
     eng = crdt_amd.Engine(B, 32, device=gpu)
     t0 = time.time()
@@ -497,7 +508,11 @@ def run_config4(args, world: int, rank: int, gpu: int, dist):
         hip.hipEventCreate(C.byref(e_))
     s_ = C.c_void_p(eng.stream())
 
-    def step(ms):
+    def step(ms, check=False):
+        """one pass over the rank's batches; check (untimed warm-up only): every batch's statuses
+        are read back and must all be OK (a batch stopped on capacity still publishes a
+        digest, of a partial state)"""
+        good = True
         for k, (b0, m) in enumerate(batches):
             eng.reseed_random_async(args.seed, b0)
             eng.reset_async()
@@ -506,14 +521,18 @@ def run_config4(args, world: int, rank: int, gpu: int, dist):
             hip.hipEventRecord(ev[1], s_)
             eng.publish_async()
             eng.digests_dev_async(d_dg.data_ptr() + 8 * k * B)
+            if check:
+                good = good and bool((eng.status() == 0).all())
             if ms is not None:
                 hip.hipEventSynchronize(ev[1])
                 x = C.c_float()
                 hip.hipEventElapsedTime(C.byref(x), ev[0], ev[1])
                 ms.append(x.value)
+        return good
 
-    for _ in range(args.warmup):
-        step(None)
+    warm_ok = True
+    for _ in range(warmup):
+        warm_ok = step(None, check=True) and warm_ok
     eng.sync()
     torch.cuda.synchronize()
     ref = d_dg.cpu().numpy().view(np.uint64).copy()  # (the warm-up pass's digests)
@@ -523,7 +542,7 @@ def run_config4(args, world: int, rank: int, gpu: int, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step(replay_ms)
     eng.sync()
     torch.cuda.synchronize()
@@ -532,36 +551,48 @@ def run_config4(args, world: int, rank: int, gpu: int, dist):
     elapsed = time.perf_counter() - t_start
     got = d_dg.cpu().numpy().view(np.uint64)
     dg = np.concatenate([got[k * B:k * B + m] for k, (b0, m) in enumerate(batches)])
-    same = bool(args.warmup == 0 or np.array_equal(got, ref))
-    ok = bool((eng.status() == 0).all()) and same
+    same = bool(warmup == 0 or np.array_equal(got, ref))
+    ok = bool((eng.status() == 0).all()) and same and warm_ok
     # sampled documents of this rank against the oracle (global ids)
     threads, affinity, quota = cpu_share()
     rng = np.random.default_rng(77 + rank)
     pick = sorted(set(rng.integers(0, n, args.check_docs).tolist()) | {0, n - 1})
     odg = oracle_digests_random(args, [lo + i for i in pick], threads)
     ok = ok and bool(np.array_equal(dg[pick], odg))
-    t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, dev)
-    oks = torch.tensor([1.0 if ok else 0.0], device=dev, dtype=torch.float64)
+    cdev = torch.device("cpu") if args.share_gpu else dev  # (gloo rehearsal on one GPU: CPU tensors)
+    t_max, per_rank, all_dg = reduce_over_ranks(elapsed, dg, dist, cdev)
+    # the gather's own check: this rank's slice of the gathered digests is what it computed
+    lo_all = [shard_balanced(np.ones(D), world, r)[0] for r in range(world)]
+    gathered_local = bool(np.array_equal(all_dg[lo_all[rank]:lo_all[rank] + n], dg))
+    oks = torch.tensor([1.0 if ok else 0.0, 1.0 if gathered_local else 0.0], device=cdev, dtype=torch.float64)
     if dist is not None:
         dist.all_reduce(oks, op=dist.ReduceOp.MIN)
-    ok = bool(oks.item() == 1.0) and int(all_dg.shape[0]) == D
+    gathered_local = bool(oks[1].item() == 1.0)
+    ok = bool(oks[0].item() == 1.0) and gathered_local and int(all_dg.shape[0]) == D
     nb = len(batches)
     rms = float(np.mean(replay_ms)) if replay_ms else None  # per k_replay launch (one batch)
-    docs_done = D * args.steps
+    docs_done = D * steps
     value = docs_done * args.gen_ops / t_max
     alg_launch = (32 * int(canon.sum()) + 24 * n * args.gen_ops) / nb  # SURVEY 8(d), per launch (batch)
+    # compulsory bytes only: the 16 B of op input per op are never read (the ops are generated in
+    # the wave), so the state written (32 B per canonical span) + 8 B of result per op remain
+    comp_launch = (32 * int(canon.sum()) + 8 * n * args.gen_ops) / nb
     achieved = alg_launch / (rms * 1e-3) / 1e9 if rms else None
+    eng.close()
+    del d_dg
+    torch.cuda.empty_cache()
+    line = None
     if rank == 0:
         cpu = None
         if not args.no_cpu:
-            cd, csec = cpu_baseline_random(args, threads, args.cpu_seconds)
+            cd, csec = cpu_baseline_random(args, threads, cpu_s)
             cpu = {"value": cd * args.gen_ops / csec, "unit": "ops/s", "cores": threads, "threads_used": threads,
                    "host_cores": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "kind": "port",
                    "sample": f"{cd} corpus documents x {args.gen_ops} generated ops on the oracle (reference B-tree "
                              f"restatement, SplitList order index), {threads} threads, one document per task, {csec:.1f} s"}
-        print(json.dumps({
+        line = {
             "metric": "CRDT ops remapped+merged/sec (whole node)", "value": value, "unit": "ops/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": t_max / args.steps * 1e3,
+            "steps": steps, "warmup": warmup, "ms_per_step": t_max / steps * 1e3,
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u32",
             "data": "synthetic: make_random_change semantics (doc.rs:544-569) generated in the replay wave",
             "config": {"workload": f"config4: {D} docs x {args.gen_ops} random-edit ops, document-sharded over "
@@ -571,6 +602,10 @@ def run_config4(args, world: int, rank: int, gpu: int, dist):
                        "waves_per_simd": B / SIMDS, "hbm_bytes_per_batch_doc": mem / B, "hbm_bytes": mem},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None,
+                         "frac_compulsory": comp_launch / (rms * 1e-3) / 1e9 / HBM_PEAK_GBS if rms else None,
+                         "compulsory_bytes_per_launch": comp_launch,
+                         "compulsory_note": "SURVEY 8(d) without the 16 B/op input term: the ops are generated in the "
+                                            "wave and never read from HBM",
                          "traffic": measured_traffic(B, "k_replay", "config4"), "kernel": "k_replay<32>",
                          "kernel_ms": rms, "alg_bytes_per_launch": alg_launch,
                          "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops), per batch launch",
@@ -580,9 +615,12 @@ def run_config4(args, world: int, rank: int, gpu: int, dist):
             "parity": f"all {D} documents' digests equal across the warm-up and timed passes; "
                       f"{len(pick)} sampled documents per rank == the oracle's replay (global document ids)",
             "world_size": dist.get_world_size() if dist is not None else 1,
-            "per_rank_ops_s": [n * args.gen_ops * args.steps / t for t in per_rank],
+            "collective": {"backend": dist.get_backend() if dist is not None else None,
+                           "gathered_docs": int(all_dg.shape[0]), "gathered_equal_local": gathered_local},
+            "per_rank_ops_s": [n * args.gen_ops * steps / t for t in per_rank],
             "build_id": crdt_amd.build_id(), "stage_s": stage_s,
-        }))
+        }
+    return line
 
 
 # ------------------------------------------------------------------------------------------------
@@ -609,6 +647,13 @@ def main():
     ap.add_argument("--gen-ops", type=int, default=20_000, help="config4: generated ops per document")
     ap.add_argument("--seed", type=int, default=0xC0FFEE, help="config4: corpus seed")
     ap.add_argument("--check-docs", type=int, default=64, help="config4: sampled documents per rank checked against the oracle")
+    ap.add_argument("--no-corpus", action="store_true",
+                    help="config2: skip the corpus leg (the 1 M-document config-4 corpus, the line's `corpus` object)")
+    ap.add_argument("--corpus-steps", type=int, default=2, help="config2: timed passes over the corpus in its leg")
+    ap.add_argument("--corpus-warmup", type=int, default=1, help="config2: untimed passes over the corpus in its leg")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the RCCL (nccl) process group even at world size 1 (under torchrun "
+                         "--nproc-per-node=1, or standalone on 127.0.0.1): the digest gather runs over RCCL")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the multi-rank path on one GPU: every rank runs its engine on cuda:0 and "
                          "the collectives go over gloo (CPU tensors); not a scaling measurement")
@@ -640,12 +685,19 @@ def main():
         print(f"bench.py: {world} rank(s) need {need} GPU(s); {torch.cuda.device_count()} visible", file=sys.stderr)
         sys.exit(2)
     gpu = 0 if args.share_gpu else local_rank
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
+        if world == 1:  # (standalone --dist: a one-rank group on the loopback address)
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(gpu)
-        dist.init_process_group("gloo" if args.share_gpu else "nccl")
+        dist.init_process_group("gloo" if args.share_gpu else "nccl", device_id=None if args.share_gpu else torch.device("cuda", gpu))
     if args.workload == "config4":
-        run_config4(args, world, rank, gpu, dist)
+        line = run_config4(args, world, rank, gpu, dist)
+        if line is not None:
+            print(json.dumps(line))
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -751,9 +803,18 @@ def main():
     gold = int(gold, 16) if gold else None
     ok = ok and q_ok and bool((all_dg == all_dg[0]).all()) and (gold is None or int(all_dg[0]) == gold)
     mat = materialize_leg(eng, args.trace, n, hip, ev, s_) if not args.no_text else None
+    sz = eng.export_sizes(0)
+    eng.close()  # (frees the config-2 pools before the other legs allocate theirs)
+    torch.cuda.empty_cache()
     stated = None
     if world == 1 and n != 4096 and not args.no_stated_size:
         stated = stated_size_leg(args, wire, n_ops_doc, hip)
+    # the north star's corpus (BASELINE config 4: 1 M random-edit documents, document-sharded over
+    # the ranks -- strong scaling at N > 1), measured in the same run after the config-2 leg
+    corpus = None
+    if not args.no_corpus:
+        corpus = run_config4(args, world, rank, gpu, dist, steps=args.corpus_steps, warmup=args.corpus_warmup,
+                             cpu_s=args.cpu_seconds / 2)
     total_ops = n_ops_doc * int(all_dg.shape[0]) * args.steps
     value = total_ops / t_max
     ms_step = t_max / args.steps * 1e3
@@ -761,7 +822,6 @@ def main():
     # roofline of k_replay, SURVEY §8(d) algorithmic bytes for one launch = the whole trace per
     # document, starting from empty documents (S = 0): 32 B per final canonical span (16 B span
     # written + 8 B vpos/rpos + 8 B order->span) + 24 B per op (16 B op in + 8 B result out)
-    sz = eng.export_sizes(0)
     canon = sz["canon"]
     alg_bytes = n * (32 * canon + 24 * n_ops_doc)
     achieved = alg_bytes / (rms * 1e-3) / 1e9 if rms else None
@@ -810,6 +870,7 @@ def main():
             "stage_intern": "host" if args.host_intern else "device (k_intern)",
             "materialize": mat,
             "stated_size": stated,
+            "corpus": corpus,
         }
         print(json.dumps(out))
     if dist is not None:

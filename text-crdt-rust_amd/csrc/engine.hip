@@ -425,23 +425,23 @@ struct crdt_engine {
               (unsigned long long)nl, (unsigned long long)nb, (unsigned long long)nm, (unsigned long long)nc,
               (unsigned long long)na, (unsigned long long)ndl, (unsigned long long)ndd, (unsigned long long)nt,
               (unsigned long long)npar, (unsigned long long)nag, (unsigned long long)nfr, np.bytes / 1e6);
-    // From here on the engine's state changes pool by pool: until the last pool has moved, a
-    // failure leaves it poisoned (and frees what this call allocated).
-    poisoned = true;
     DocSeg* old_segs = nullptr;
     struct Cleanup {
       PoolSet& np;
       DocSeg*& os;
       ~Cleanup() { dfree(np.agents); dfree(os); }
     } cleanup{np, old_segs};
+    // The two allocations come before any engine state changes: an out-of-memory error here
+    // leaves the engine intact (the caller may free memory and retry).
     HIPCHK(dalloc(np.agents, nag));  // (the new agent table first: the run move reads its bases)
+    if (move) HIPCHK(dalloc(old_segs, n_docs));
+    // From here on the engine's state changes pool by pool: until the last pool has moved, a
+    // failure leaves it poisoned (and frees what this call allocated).
+    poisoned = true;
     if (!agent_tab.empty())
       HIPCHK(hipMemcpyAsync(np.agents, agent_tab.data(), agent_tab.size() * sizeof(AgentRec), hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemcpyAsync(n_agents_d, n_agents.data(), n_docs * 4, hipMemcpyHostToDevice, stream));
-    if (move) {
-      HIPCHK(dalloc(old_segs, n_docs));
-      HIPCHK(hipMemcpyAsync(old_segs, segs, n_docs * sizeof(DocSeg), hipMemcpyDeviceToDevice, stream));
-    }
+    if (move) HIPCHK(hipMemcpyAsync(old_segs, segs, n_docs * sizeof(DocSeg), hipMemcpyDeviceToDevice, stream));
     HIPCHK(hipMemcpyAsync(segs, nseg.data(), n_docs * sizeof(DocSeg), hipMemcpyHostToDevice, stream));
     // Pool by pool: allocate the new one, move every document's part (k_relayout_pool), free the
     // old one.  The peak is the old pools + the largest new pool (2x both sets before).  A pool
@@ -964,8 +964,16 @@ struct crdt_engine {
     HIPCHK(hipMemcpy(cn.data(), canon_n, n_docs * 4, hipMemcpyDeviceToHost));
     for (u64 d = 0; d < n_docs; d++) {
       const DocState& s = st_h[d];
-      if (s.status != ST_OK) continue;
       DocHost& h = docs[d];
+      if (s.status != ST_OK) {
+        // (its state says nothing about its needs; mode 2 still applies and forgets what earlier
+        // notes gathered, so no stale maximum carries into the next note cycle)
+        if (mode == 2 && h.fit_noted) {
+          caps_max(h.caps, h.fit_max);
+          h.fit_noted = false;
+        }
+        continue;
+      }
       const StreamNeeds& m = h.cum;
       Caps fc = h.caps;
       Caps& c = mode == 0 ? h.caps : fc;
@@ -1703,6 +1711,10 @@ int crdt_digest_dev_async(crdt_engine* e, uint64_t* dev_out) {
   if (!valid(e) || !dev_out) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
+  if (!e->published) {  // (the digests are publish's: never hand out the previous replay's)
+    r = e->publish();
+    if (r) return r;
+  }
   HIPCHK(hipMemcpyAsync(dev_out, e->digest, e->n_docs * 8, hipMemcpyDeviceToDevice, e->stream));
   return 0;
 }
