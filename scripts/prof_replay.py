@@ -93,4 +93,7 @@ if a.clean:
 else:
     e.publish_async()
     e.sync()
-print("status ok:", bool((st == 0).all()), "replay_ms", replay_ms, "pub_ms", pub_ms, "wall", time.time() - t0)
+import hashlib  # noqa: E402
+dg = e.digests()
+print("status ok:", bool((st == 0).all()), "replay_ms", replay_ms, "pub_ms", pub_ms, "wall", time.time() - t0,
+      "digests", hashlib.sha256(dg.tobytes()).hexdigest()[:12])

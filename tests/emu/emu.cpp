@@ -164,7 +164,13 @@ struct EmuDoc {
       Replayer<WaveCPU<LL>, LL> r(p, 0);
       if (first) { r.init_empty(); r.p(S_N_AGENTS, (u32)agents.names.size()); first = false; }
       else { r.p(S_STATUS, (u32)ST_OK); r.begin(); }
-      r.run();
+      // the stream's shape picks the run<> instance, as the engine picks a k_replay instance
+      u32 kinds = 0;
+      for (const Rec& x : recs) kinds |= 1u << rec_kind(x);
+      u32 sh = shape_of_kinds(kinds);
+      if (sh == SHAPE_REMOTE) r.template run<SHAPE_REMOTE>();
+      else if (sh == SHAPE_GEN) r.template run<SHAPE_GEN>();
+      else r.template run<SHAPE_ALL>();
       r.finish();
       if (st.status != ST_NEED_CAPACITY) break;
       if (st.cap_need == 0 || ((st.cap_need & 1u) && seg.leaf_cap >= MAX_LEAVES) || grow_events > 64) {

@@ -5,6 +5,7 @@ len < 100 else 0.45; insert 1 char at U[0, len]; delete U[1, min(10, len-pos)] a
 concurrent_wire: several agents editing their own replicas (oracle) and exchanging remote txns;
 returns one causally ordered wire batch that replays the whole history.
 """
+import os
 import random
 import struct
 
@@ -221,3 +222,48 @@ def config1_probes(counts, patches, agent: int, seed=None):
         pr[k, 0] = rng.integers(0, np.maximum(p[first_op[k], 0] + 3, 1))
         pr[k, 2] = rng.integers(0, seq0[k] + txn_len[k])
     return pr.astype(np.uint32)
+
+
+_GEN = None
+
+
+def _gen_lib():
+    """tests/gen/build/libgen.so (C++ config-5 history generator; built on first use)."""
+    global _GEN
+    if _GEN is None:
+        import ctypes as C
+        import fcntl
+        import subprocess
+        d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gen")
+        os.makedirs(os.path.join(d, "build"), exist_ok=True)
+        with open(os.path.join(d, "build", ".lock"), "w") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            subprocess.run(["make", "-s", "-C", d], check=True)
+        L = C.CDLL(os.path.join(d, "build", "libgen.so"))
+        L.c5_gen_batch.argtypes = [C.c_uint64, C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   C.c_uint32, C.c_double, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64)]
+        L.c5_free.argtypes = [C.c_void_p]
+        _GEN = L
+    return _GEN
+
+
+def config5_wires(seeds, base_len: int = 1 << 20, n_agents: int = 16, rounds: int = 64, ops: int = 64,
+                  hot: int = 32, del_frac: float = 0.6, threads: int = 8):
+    """BASELINE config 5 histories from the C++ generator (tests/gen/config5_gen.cpp): the shape of
+    config5_wire above, one history per seed (its own ops and its own delivery interleaving),
+    generated on `threads` threads.  Returns a list of wire batches (bytes)."""
+    import ctypes as C
+    L = _gen_lib()
+    sd = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))
+    n = int(sd.shape[0])
+    ptr = (C.c_void_p * n)()
+    ln = np.zeros(n, np.uint64)
+    rc = L.c5_gen_batch(n, sd.ctypes.data_as(C.POINTER(C.c_uint64)), base_len, n_agents, rounds, ops, hot, del_frac,
+                        threads, ptr, ln.ctypes.data_as(C.POINTER(C.c_uint64)))
+    if rc != 0:
+        raise ValueError("c5_gen_batch: bad parameters")
+    out = []
+    for i in range(n):
+        out.append(C.string_at(ptr[i], int(ln[i])))
+        L.c5_free(ptr[i])
+    return out

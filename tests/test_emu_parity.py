@@ -145,6 +145,31 @@ def test_config5_full_size(L):
     assert e.sizes()["frontier"] == 16 and e.sizes()["grow_mask"] & 128
 
 
+def test_config5_generator_histories():
+    # the C++ config-5 generator (tests/gen, scripts/bench_config5.py --distinct): every seed gives
+    # its own causally ordered history (the oracle replays it with status OK), seeds differ, a seed
+    # repeats exactly, and the replay core equals the oracle on small histories at both layouts and
+    # on one history of SURVEY's full shape (1 M-char base, 16 agents x 64 rounds x 64 txns)
+    from fuzz_gen import config5_wires
+    ws = config5_wires([11, 12, 11], base_len=4096, n_agents=16, rounds=6, ops=4)
+    assert ws[0] == ws[2] and ws[0] != ws[1]
+    for w in ws[:2]:
+        for L in (32, 4):
+            o = OracleDoc(L, 16 if L == 32 else 8)
+            assert o.apply_remote_wire(w) == 0
+            e = EmuDoc(L)
+            assert e.run_wire(w, 48) == 0
+            assert e.check() == ""
+            assert diff_states(o.export(), e.export()) == []
+    w = config5_wires([5])[0]
+    o = OracleDoc(32, 16)
+    assert o.apply_remote_wire(w) == 0
+    assert o.sizes()["dd"] > 0  # overlapping deletes made double deletes
+    e = EmuDoc(32)
+    assert e.run_wire(w, 48) == 0
+    assert diff_states(o.export(), e.export()) == []
+
+
 @pytest.mark.parametrize("name", ["sveltecomponent", "automerge-paper"])
 @pytest.mark.parametrize("L", [32, 4])
 def test_config1_probes(name, L):

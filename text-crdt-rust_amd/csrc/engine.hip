@@ -111,6 +111,7 @@ struct DocHost {
   bool fit_noted = false;
   bool tracked = false;     // keeps the order -> leaf map (once a remote stream was staged)
   bool agent_map = false;   // keeps the order -> agent map (tracked, and more than one agent)
+  u32 shape = SHAPE_ALL;    // record kinds of the staged stream (crdt_types.h SHAPE_*): its k_replay instance
   std::vector<u32> agent_cap;
 };
 
@@ -203,7 +204,7 @@ struct crdt_engine {
   u32* n_agents_d = nullptr;
   std::vector<u32> n_agents_pushed;  // host copy of what n_agents_d holds
   // replay launches: one per LDS root class present; `doc_list` holds the classes' documents
-  struct RootClass { u32 rcap; u64 off, n; bool hr; };
+  struct RootClass { u32 rcap; u64 off, n; bool hr; u32 shape; };
   std::vector<RootClass> classes;
   u32* doc_list = nullptr;
   PoolSet pools;
@@ -582,26 +583,36 @@ struct crdt_engine {
   // Replay launch classes (LDS root sizes) from the documents' root capacities; the documents
   // of every class go to the device list when more than one class is present.
   int plan_classes() {
-    // classes 0-3: the LDS root sizes; class 4: the two-level root (top size: the largest needed)
-    std::vector<std::vector<u32>> by(5);
+    // classes 0-3: the LDS root sizes; class 4: the two-level root (top size: the largest needed);
+    // the LDS-root classes split further by stream shape (one k_replay instance per shape), bucket
+    // k * N_SHAPES + shape; the two-level root has one instance (SHAPE_ALL), bucket 4 * N_SHAPES
+    std::vector<std::vector<u32>> by(4 * N_SHAPES + 1);
     u32 hr_top = 64;
+    // documents with nothing to replay go with the shape of the first one that has a stream (no
+    // launch of their own: they return at once in any instance)
+    u32 sh0 = SHAPE_ALL;
+    for (u64 d = 0; d < n_docs; d++)
+      if (seg_h[d].rec_n) { sh0 = docs[d].shape; break; }
     for (u64 d = 0; d < n_docs; d++) {
       u32 gc = seg_h[d].grp_cap;
       if (uses_hroot(gc)) {
-        by[4].push_back((u32)d);
+        by[4 * N_SHAPES].push_back((u32)d);
         hr_top = std::max(hr_top, hroot_top(gc));
         continue;
       }
       u32 c = root_class(gc);
       u32 k = 0;
       while (ROOT_CLASSES[k] != c) k++;
-      by[k].push_back((u32)d);
+      by[k * N_SHAPES + (seg_h[d].rec_n ? docs[d].shape : sh0)].push_back((u32)d);
     }
     if (hr_top > ROOT_CAP_MAX) {
       g_last_error = "a document's root exceeds the two-level root's top level";
       return CRDT_E_NOMEM;
     }
-    auto rc = [&](u32 k) { return k < 4 ? ROOT_CLASSES[k] : hr_top; };
+    auto rc = [&](u32 b) { return b < 4 * N_SHAPES ? ROOT_CLASSES[b / N_SHAPES] : hr_top; };
+    auto cls = [&](u32 b, u64 off, u64 n) {
+      return RootClass{rc(b), off, n, b == 4 * N_SHAPES, b < 4 * N_SHAPES ? b % N_SHAPES : (u32)SHAPE_ALL};
+    };
     // Within a class the longest staged streams launch first (LPT order): a workgroup's waves hold
     // their slots until its last one ends, so workgroups of similar documents, longest first, leave
     // the short ones to fill the end of the launch (mixed corpora: config 3).  Equal streams keep
@@ -623,14 +634,14 @@ struct crdt_engine {
     u32 present = 0;
     for (auto& v : by) present += !v.empty();
     if (present <= 1 && identity) {
-      for (u32 k = 0; k < 5; k++)
-        if (!by[k].empty()) classes.push_back(RootClass{rc(k), INVALID, by[k].size(), k == 4});
+      for (u32 k = 0; k < by.size(); k++)
+        if (!by[k].empty()) classes.push_back(cls(k, INVALID, by[k].size()));
       return 0;
     }
     std::vector<u32> all;
-    for (u32 k = 0; k < 5; k++) {
+    for (u32 k = 0; k < by.size(); k++) {
       if (by[k].empty()) continue;
-      classes.push_back(RootClass{rc(k), all.size(), by[k].size(), k == 4});
+      classes.push_back(cls(k, all.size(), by[k].size()));
       all.insert(all.end(), by[k].begin(), by[k].end());
     }
     HIPCHK(dalloc(doc_list, all.size()));
@@ -728,6 +739,22 @@ struct crdt_engine {
         pulled = true;
       }
       if (st_h[doc_ids[i]].next_order) rebuild_ag.push_back((u32)doc_ids[i]);
+    }
+    // stream shapes: the record kinds of each distinct host stream (k_replay instance per shape;
+    // CRDT_NO_SHAPES=1 in the environment keeps every stream on the general instance, for A/B)
+    {
+      static const bool no_shapes = getenv("CRDT_NO_SHAPES") && getenv("CRDT_NO_SHAPES")[0] == '1';
+      std::unordered_map<const std::vector<Rec>*, u32> kinds_of;
+      for (u64 d = 0; d < n_docs; d++) docs[d].shape = SHAPE_ALL;
+      for (size_t i = 0; i < doc_ids.size(); i++) {
+        auto f = kinds_of.find(streams[i]);
+        if (f == kinds_of.end()) {
+          u32 k = 0;
+          for (const Rec& x : *streams[i]) k |= 1u << rec_kind(x);
+          f = kinds_of.emplace(streams[i], k).first;
+        }
+        docs[doc_ids[i]].shape = no_shapes ? (u32)SHAPE_ALL : shape_of_kinds(f->second);
+      }
     }
     // cumulative needs -> capacities
     for (size_t i = 0; i < doc_ids.size(); i++) {
@@ -882,9 +909,16 @@ struct crdt_engine {
       if (c.hr) {
         if (L == 32) hipLaunchKernelGGL(k_replay_hr<32>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
         else hipLaunchKernelGGL(k_replay_hr<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
-      } else {
-        if (L == 32) hipLaunchKernelGGL(k_replay<32>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
-        else hipLaunchKernelGGL(k_replay<4>, dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+      } else {  // (one instance per stream shape)
+        if (L == 32) {
+          if (c.shape == SHAPE_REMOTE) hipLaunchKernelGGL((k_replay<32, SHAPE_REMOTE>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+          else if (c.shape == SHAPE_GEN) hipLaunchKernelGGL((k_replay<32, SHAPE_GEN>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+          else hipLaunchKernelGGL((k_replay<32, SHAPE_ALL>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+        } else {
+          if (c.shape == SHAPE_REMOTE) hipLaunchKernelGGL((k_replay<4, SHAPE_REMOTE>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+          else if (c.shape == SHAPE_GEN) hipLaunchKernelGGL((k_replay<4, SHAPE_GEN>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+          else hipLaunchKernelGGL((k_replay<4, SHAPE_ALL>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+        }
       }
       HIPCHK(hipGetLastError());
     }
@@ -1214,8 +1248,12 @@ int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
   if (hipSetDevice(e->device) != hipSuccess) return CRDT_E_DEVICE;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return CRDT_E_DEVICE;
   // the replay's LDS root may take a workgroup's whole 160 KiB (one wave per workgroup)
-  (void)hipFuncSetAttribute((const void*)k_replay<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)k_replay<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<32, SHAPE_ALL>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<4, SHAPE_ALL>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<32, SHAPE_REMOTE>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<4, SHAPE_REMOTE>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<32, SHAPE_GEN>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<4, SHAPE_GEN>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay_hr<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay_hr<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<32>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void k_init(Pools P, u32 n, u32 wpb, u32 rcap)
 // documents in 185 ms where the compiler's own choice (84 VGPRs: 5 waves/SIMD) takes 199 ms and
 // 97 VGPRs (4 waves/SIMD) took 216 ms (scripts/gpu_ab.sh).  What the budget costs is a few spills
 // in cold paths.
-template <int L, bool HR>
+template <int L, bool HR, u32 SH = SHAPE_ALL>
 __device__ __forceinline__ void replay_doc(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
   u32 d;
   if (!wave_doc(wpb, list, n, d)) return;
@@ -102,15 +102,17 @@ __device__ __forceinline__ void replay_doc(Pools P, u32 n, u32 wpb, u32 rcap, co
     return;
   }
   r.begin();
-  r.run();
+  r.template run<SH>();
   r.finish();
 }
 #ifndef CRDT_REPLAY_WAVES
 #define CRDT_REPLAY_WAVES 8  // waves per SIMD the replay's register budget is held to (diagnostic builds vary it)
 #endif
-template <int L>
+// SH: the stream shape of every document of the launch (crdt_types.h SHAPE_*; the host launches
+// each shape's documents in their own instance: SHAPE_ALL is the general one)
+template <int L, u32 SH>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRDT_REPLAY_WAVES))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
-  replay_doc<L, false>(P, n, wpb, rcap, list);
+  replay_doc<L, false, SH>(P, n, wpb, rcap, list);
 }
 // Documents past the LDS root replay with the two-level root (wave_gpu.h HR).  They are few and
 // long, so this instance is held to 4 waves per SIMD (<= 128 VGPRs: no scratch for its extra

@@ -130,6 +130,9 @@ struct Replayer {
   // op fetch + origins + insert_internal), added to the DocState counters of d % 4 == 3 documents
   u32 pt_scan = 0, pt_del = 0, pt_ins = 0;
 #endif
+#ifdef CRDT_EMU_STATS
+  u32 st_prev_leaf = INVALID;  // (statistics build: the leaf cached before the current one)
+#endif
 
   // ------------------------------------------------------------------ context access
   CRDT_HD u32 g(u32 f) const { return w.xg(f); }
@@ -408,6 +411,10 @@ struct Replayer {
   // the leaf's entries are requested before the slot is first used, so both arrive together.
   // `succ`: its successor leaf if the caller has it (INVALID: not known yet).
   CRDT_HD void load_cache(u32 leaf, u32 slot, u32 succ = INVALID) {
+#ifdef CRDT_EMU_STATS  // leaf switches; 71: back to the leaf cached before the current one; 72: the current one was dirty
+    CRDT_STAT(70, 1); CRDT_STAT(71, leaf == st_prev_leaf); CRDT_STAT(72, g(C_DIRTY) != 0u);
+    st_prev_leaf = g(C_LEAF);
+#endif
     commit();
     p(C_N, w.cache_load(leafp(leaf)));
     u32 sl = w.uni_(slot);
@@ -2562,15 +2569,26 @@ struct Replayer {
 
   // Replay this document's record stream from its rec_pos.  A GEN record stays current until
   // all its ops are applied (progress in S_GEN_DONE, so a capacity stop resumes mid-record).
+  // SH (crdt_types.h SHAPE_*): the record kinds the stream may hold, known to the host at staging.
+  // A stream of remote records only (SHAPE_REMOTE: the remote-batch configs) or of GEN records
+  // only (SHAPE_GEN: config 4) replays in an instance without the other kinds' loops and without
+  // the other side of the general interpreter (apply_txn's `remote` is then a constant), so the
+  // hot loop's registers are allocated around less code.  A record of a kind the shape excludes
+  // stops the document (ST_BAD_INPUT; the host never launches such a stream in that instance).
+  template <u32 SH = SHAPE_ALL>
   CRDT_HD void run() {
+    constexpr bool any_remote = SH != SHAPE_GEN, any_local = SH != SHAPE_REMOTE;
     u32 pos = g(S_REC_POS);
     u32 rn = rec_n();
     while (pos < rn) {
       w.x_pin();
       Rec h = rec(pos);
       u32 kind = rec_kind(h);
+      if constexpr (SH != SHAPE_ALL) {
+        if (!((shape_kinds(SH) >> kind) & 1u)) { p(S_STATUS, (u32)ST_BAD_INPUT); pos += 1; break; }
+      }
       u32 tried = 0;  // the fast path already declined this record
-      if (kind == REC_RC) {
+      if (any_remote && kind == REC_RC) {
         // the remote-batch hot loop: compact remote txns through one fast-path instance, in a loop
         // of their own (its registers do not meet the other record kinds' paths at every txn)
         u32 fast;
@@ -2597,7 +2615,7 @@ struct Replayer {
         }
         if (pos >= rn) break;
         tried = kind == REC_RC ? 1u : 0u;
-      } else if (kind == REC_LC) {
+      } else if (SH == SHAPE_ALL && kind == REC_LC) {
         // the same for compact local txns (local-trace corpora: configs 1 and 3)
         while (true) {
 #ifdef CRDT_PROF
@@ -2633,7 +2651,7 @@ struct Replayer {
         }
         if (pos >= rn) break;
         tried = kind == REC_LC ? 1u : 0u;
-      } else if (kind == REC_GEN) {
+      } else if (any_local && kind == REC_GEN) {
         // generated ops (config 4) in a loop of their own: gen_op and one fast-path instance per
         // op, no trip through the record window and the kind dispatch
         // The draws of 64 ops at a time are computed lane-parallel into the record window's
@@ -2683,7 +2701,7 @@ struct Replayer {
         p(S_GEN_DONE, done);
         tried = 1u;  // (the general path takes op `done`, or the record ends below)
       }
-      u32 gen = opq(kind == REC_GEN ? 1u : 0u);
+      u32 gen = any_local ? opq(kind == REC_GEN ? 1u : 0u) : 0u;
       Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
       u32 inl = 0;
       if (gen) {  // (F_GEN carries the flag past the txn: no register lives across the loop body)
@@ -2707,6 +2725,7 @@ struct Replayer {
         // (a general remote txn by another author than the cached one, or with several frontier
         // heads, fails fast_txn_ok at once: skip the attempt's record decoding)
         if (kind == REC_RTXN) tried |= (((h.w1 & 0xFFFFu) != g(T_AG_ID)) | (g(S_N_FR) != 1u)) ? 1u : 0u;
+        if constexpr (SH == SHAPE_GEN) tried = 1u;  // (only synthesized generated ops get here: tried in the GEN loop)
         u32 fast = tried ? 0u : fast_txn(pos, kind, 0u, h, gop);  // (a GEN record was tried above)
 #ifdef CRDT_PROF
         u64 t1 = w.clock();
@@ -2722,9 +2741,9 @@ struct Replayer {
           else pos += fast;
           continue;
         }
-        bool remote = ((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u;
-        if (kind == REC_RC) { expand_rc(h, h, gop, gpar); inl = 1; }
-        if (kind == REC_LC) { expand_lc(h, h, gop); inl = 1; }
+        bool remote = SH == SHAPE_REMOTE ? true : SH == SHAPE_GEN ? false : (((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u);
+        if (any_remote && kind == REC_RC) { expand_rc(h, h, gop, gpar); inl = 1; }
+        if (SH == SHAPE_ALL && kind == REC_LC) { expand_lc(h, h, gop); inl = 1; }
         u32 nops = remote ? (h.w0 & RTXN_NOPS_MASK) : (h.w0 & 0x0FFFFFFFu);
         consumed = inl ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, inl, gop, gpar) : ST_BAD_INPUT;
@@ -2732,7 +2751,7 @@ struct Replayer {
 #ifdef CRDT_PROF
         if (prof_mode != 3u) inc(S_PROF1, prof_mode == 0u ? (u32)(w.clock() - t1) : 1u);
 #endif
-      } else if (kind == REC_PROBE) {
+      } else if (SH == SHAPE_ALL && kind == REC_PROBE) {
         probe(h, pos);
         st = ST_OK;
         consumed = 1;
