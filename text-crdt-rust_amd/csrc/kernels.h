@@ -110,8 +110,11 @@ __device__ __forceinline__ void replay_doc(Pools P, u32 n, u32 wpb, u32 rcap, co
 #endif
 // SH: the stream shape of every document of the launch (crdt_types.h SHAPE_*; the host launches
 // each shape's documents in their own instance: SHAPE_ALL is the general one)
+#ifndef CRDT_REPLAY_WAVES_GEN
+#define CRDT_REPLAY_WAVES_GEN CRDT_REPLAY_WAVES  // (the generated-op instance's budget; diagnostic builds vary it)
+#endif
 template <int L, u32 SH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRDT_REPLAY_WAVES))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SH == SHAPE_GEN ? CRDT_REPLAY_WAVES_GEN : CRDT_REPLAY_WAVES))) void k_replay(Pools P, u32 n, u32 wpb, u32 rcap, const u32* list) {
   replay_doc<L, false, SH>(P, n, wpb, rcap, list);
 }
 // Documents past the LDS root replay with the two-level root (wave_gpu.h HR).  They are few and
