@@ -9,6 +9,7 @@ for w in ${WL:-ap c4}; do
     ap) ARGS="--docs 8192 --clean";;
     c4) ARGS="--docs 16384 --random 20000 --clean";;
     c4b) ARGS="--docs 125000 --random 20000 --clean";;
+    apl) ARGS="--docs 8192 --local --clean";;
     c3) ARGS="--docs 65536 --config3 --clean --no-fit";;
     c5) ARGS="--docs 4096 --config5 --clean";;
     j1) ARGS="--docs 2048 --clean --wire data/micro/jump1.rtx.gz";;

@@ -170,6 +170,7 @@ struct EmuDoc {
       u32 sh = shape_of_kinds(kinds);
       if (sh == SHAPE_REMOTE) r.template run<SHAPE_REMOTE>();
       else if (sh == SHAPE_GEN) r.template run<SHAPE_GEN>();
+      else if (sh == SHAPE_LOCAL) r.template run<SHAPE_LOCAL>();
       else r.template run<SHAPE_ALL>();
       r.finish();
       if (st.status != ST_NEED_CAPACITY) break;

@@ -39,11 +39,11 @@ def test_no_cpu_fallback():
 def test_codegen_guard_holds_for_the_built_library():
     # build() refuses a library whose replay kernel leaves the 8-waves/SIMD register budget
     # (<= 64 VGPRs, no spill written inside the replay loop): the built one passes, at both leaf
-    # layouts and for every stream-shape instance (crdt_types.h SHAPE_*: all, remote, generated)
+    # layouts and for every stream-shape instance (crdt_types.h SHAPE_*: all, remote, generated, local)
     crdt_amd.build()
     seen = crdt_amd.check_codegen(crdt_amd.LIB_PATH)
     replay = [r for n, r in seen.items() if "8k_replayI" in n]
-    assert len(replay) == 2 * 3
+    assert len(replay) == 2 * 4
     for r in replay:
         assert r["vgpr_count"] <= 64 and r.get("private_segment_fixed_size", 0) <= 32
     # (at most one spill slot, written outside the replay loop)

@@ -196,16 +196,18 @@ struct Rec { u32 w0, w1, w2, w3; };
 CRDT_HD u32 rec_kind(const Rec& r) { return r.w0 >> 28; }
 // Stream shapes (Replayer::run<SH>): which record kinds a document's staged stream holds.  The
 // host classifies every stream at staging and launches each shape in its own k_replay instance.
-enum : u32 { SHAPE_ALL = 0, SHAPE_REMOTE = 1, SHAPE_GEN = 2, N_SHAPES = 3 };
+enum : u32 { SHAPE_ALL = 0, SHAPE_REMOTE = 1, SHAPE_GEN = 2, SHAPE_LOCAL = 3, N_SHAPES = 4 };
 CRDT_HD constexpr u32 shape_kinds(u32 sh) {
   return sh == SHAPE_REMOTE ? (1u << REC_RTXN | 1u << REC_RINS | 1u << REC_RDEL | 1u << REC_RPARENT | 1u << REC_RC)
        : sh == SHAPE_GEN ? (1u << REC_GEN)
+       : sh == SHAPE_LOCAL ? (1u << REC_LTXN | 1u << REC_LOP | 1u << REC_LC | 1u << REC_PROBE)
        : 0xFFFFFFFFu;
 }
 // the narrowest shape holding a stream whose record kinds are the bits of `kinds`
 inline u32 shape_of_kinds(u32 kinds) {
   if ((kinds & ~shape_kinds(SHAPE_REMOTE)) == 0u) return SHAPE_REMOTE;
   if ((kinds & ~shape_kinds(SHAPE_GEN)) == 0u) return SHAPE_GEN;
+  if ((kinds & ~shape_kinds(SHAPE_LOCAL)) == 0u) return SHAPE_LOCAL;
   return SHAPE_ALL;
 }
 // RTXN header: has_del (a delete op follows: the double-delete reserve applies, fits()) and n_ops

@@ -913,10 +913,12 @@ struct crdt_engine {
         if (L == 32) {
           if (c.shape == SHAPE_REMOTE) hipLaunchKernelGGL((k_replay<32, SHAPE_REMOTE>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
           else if (c.shape == SHAPE_GEN) hipLaunchKernelGGL((k_replay<32, SHAPE_GEN>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+          else if (c.shape == SHAPE_LOCAL) hipLaunchKernelGGL((k_replay<32, SHAPE_LOCAL>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
           else hipLaunchKernelGGL((k_replay<32, SHAPE_ALL>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
         } else {
           if (c.shape == SHAPE_REMOTE) hipLaunchKernelGGL((k_replay<4, SHAPE_REMOTE>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
           else if (c.shape == SHAPE_GEN) hipLaunchKernelGGL((k_replay<4, SHAPE_GEN>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
+          else if (c.shape == SHAPE_LOCAL) hipLaunchKernelGGL((k_replay<4, SHAPE_LOCAL>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
           else hipLaunchKernelGGL((k_replay<4, SHAPE_ALL>), dim3(blocks), dim3(64 * sh.wpb), sh.lds, stream, pv, (u32)c.n, sh.wpb, sh.rcap, list);
         }
       }
@@ -1253,7 +1255,9 @@ int crdt_engine_create(const crdt_cfg* cfg, crdt_engine** out) {
   (void)hipFuncSetAttribute((const void*)k_replay<32, SHAPE_REMOTE>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay<4, SHAPE_REMOTE>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay<32, SHAPE_GEN>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<32, SHAPE_LOCAL>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay<4, SHAPE_GEN>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)k_replay<4, SHAPE_LOCAL>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay_hr<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_replay_hr<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)k_pos_to_loc_blk<32>, hipFuncAttributeMaxDynamicSharedMemorySize, QBLK_LDS);

@@ -277,6 +277,9 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
 // wave, each wave compacts its range, the spans that cross range boundaries are resolved once,
 // and the index sweeps are split over the waves.
 // ---------------------------------------------------------------------------------------------
+#ifndef PUB_DEPTH
+#define PUB_DEPTH 1  // compaction steps whose leaf loads are in flight at once (compact_range)
+#endif
 #define PUB_BIG_WAVES 16
 #define PUB_BIG_MIN 2048u        // leaves from which a document may publish with a workgroup ...
 #define PUB_BIG_FEW_DOCS 1024u   // ... when the batch has at most this many documents
@@ -350,10 +353,27 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
       u32 leaf = shfl(mydl, li < iend ? li : 0u);
       return li < iend ? *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1))) : uint4{0, 0, 0, 0};
     };
+    // PUB_DEPTH steps of loads in flight (Little's law: one wave's 1 KiB per step is too little to
+    // cover HBM latency at 8 waves per SIMD)
     uint4 vn = ld(i0);
+#if PUB_DEPTH >= 2
+    uint4 vn2 = i0 + PER < iend ? ld(i0 + PER) : uint4{0, 0, 0, 0};
+#endif
+#if PUB_DEPTH >= 3
+    uint4 vn3 = i0 + 2u * PER < iend ? ld(i0 + 2u * PER) : uint4{0, 0, 0, 0};
+#endif
     for (u32 i = i0; i < iend; i += PER) {
       uint4 v = vn;
+#if PUB_DEPTH >= 3
+      vn = vn2;
+      vn2 = vn3;
+      if (i + 3u * PER < iend) vn3 = ld(i + 3u * PER);
+#elif PUB_DEPTH >= 2
+      vn = vn2;
+      if (i + 2u * PER < iend) vn2 = ld(i + 2u * PER);
+#else
       if (i + PER < iend) vn = ld(i + PER);
+#endif
       u64 VM = ballot(v.w != 0u);
       u32 nn = (u32)__popcll(VM);
       if (PER > 1) {
@@ -618,15 +638,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   u32 out = 0, vis = 0;
   RangeSum sum{};
   u64 h = 0;
+#ifdef PUB_NO_DIGEST  // (diagnostic: what the digest costs inside k_publish)
+  compact_range<L, true, false>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, O.corder + seg.canon_base, seg.canon_cap,
+                                out, vis, 0u, 0, sum, h, s_ring[threadIdx.x >> 6]);
+#else
   compact_range<L, true, true>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, O.corder + seg.canon_base, seg.canon_cap,
                                out, vis, 0u, 0, sum, h, s_ring[threadIdx.x >> 6]);
+#endif
   if (out > seg.canon_cap) {  // canonical spans beyond the planned capacity: report, never write past it
     if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (pub_words(seg.ord_cap) > xw) h += publish_index<1, false>(O, seg, s, canon, out, 0u, nullptr);
+#ifndef PUB_NO_DIGEST
   h += digest_tables<L>(P, seg, s, w);
+#endif
   h = wave_sum64(h);
   if (l == 0) {
     O.canon_n[d] = out;

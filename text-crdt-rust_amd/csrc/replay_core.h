@@ -2577,7 +2577,8 @@ struct Replayer {
   // stops the document (ST_BAD_INPUT; the host never launches such a stream in that instance).
   template <u32 SH = SHAPE_ALL>
   CRDT_HD void run() {
-    constexpr bool any_remote = SH != SHAPE_GEN, any_local = SH != SHAPE_REMOTE;
+    constexpr bool any_remote = SH == SHAPE_ALL || SH == SHAPE_REMOTE;
+    constexpr bool any_lc = SH == SHAPE_ALL || SH == SHAPE_LOCAL, any_gen = SH == SHAPE_ALL || SH == SHAPE_GEN;
     u32 pos = g(S_REC_POS);
     u32 rn = rec_n();
     while (pos < rn) {
@@ -2615,7 +2616,7 @@ struct Replayer {
         }
         if (pos >= rn) break;
         tried = kind == REC_RC ? 1u : 0u;
-      } else if (SH == SHAPE_ALL && kind == REC_LC) {
+      } else if (any_lc && kind == REC_LC) {
         // the same for compact local txns (local-trace corpora: configs 1 and 3)
         while (true) {
 #ifdef CRDT_PROF
@@ -2651,7 +2652,7 @@ struct Replayer {
         }
         if (pos >= rn) break;
         tried = kind == REC_LC ? 1u : 0u;
-      } else if (any_local && kind == REC_GEN) {
+      } else if (any_gen && kind == REC_GEN) {
         // generated ops (config 4) in a loop of their own: gen_op and one fast-path instance per
         // op, no trip through the record window and the kind dispatch
         // The draws of 64 ops at a time are computed lane-parallel into the record window's
@@ -2701,7 +2702,7 @@ struct Replayer {
         p(S_GEN_DONE, done);
         tried = 1u;  // (the general path takes op `done`, or the record ends below)
       }
-      u32 gen = any_local ? opq(kind == REC_GEN ? 1u : 0u) : 0u;
+      u32 gen = any_gen ? opq(kind == REC_GEN ? 1u : 0u) : 0u;
       Rec gop{0, 0, 0, 0}, gpar{0, 0, 0, 0};
       u32 inl = 0;
       if (gen) {  // (F_GEN carries the flag past the txn: no register lives across the loop body)
@@ -2741,9 +2742,10 @@ struct Replayer {
           else pos += fast;
           continue;
         }
-        bool remote = SH == SHAPE_REMOTE ? true : SH == SHAPE_GEN ? false : (((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u);
+        bool remote = SH == SHAPE_REMOTE ? true : (SH == SHAPE_GEN || SH == SHAPE_LOCAL) ? false
+                                                : (((1u << REC_RTXN | 1u << REC_RC) >> kind) & 1u);
         if (any_remote && kind == REC_RC) { expand_rc(h, h, gop, gpar); inl = 1; }
-        if (SH == SHAPE_ALL && kind == REC_LC) { expand_lc(h, h, gop); inl = 1; }
+        if (any_lc && kind == REC_LC) { expand_lc(h, h, gop); inl = 1; }
         u32 nops = remote ? (h.w0 & RTXN_NOPS_MASK) : (h.w0 & 0x0FFFFFFFu);
         consumed = inl ? 1u : 1 + nops + (remote ? (h.w1 >> 16) : 0u);
         st = (pos + consumed <= rn) ? apply_txn(h, pos, remote, inl, gop, gpar) : ST_BAD_INPUT;
@@ -2751,7 +2753,7 @@ struct Replayer {
 #ifdef CRDT_PROF
         if (prof_mode != 3u) inc(S_PROF1, prof_mode == 0u ? (u32)(w.clock() - t1) : 1u);
 #endif
-      } else if (SH == SHAPE_ALL && kind == REC_PROBE) {
+      } else if (any_lc && kind == REC_PROBE) {
         probe(h, pos);
         st = ST_OK;
         consumed = 1;
