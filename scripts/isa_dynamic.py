@@ -17,7 +17,7 @@ import os
 import re
 import sys
 
-SYM = "_ZN4crdt8k_replayILi32EEEvNS_5PoolsEjjjPKj"
+SYM = os.environ.get("ISA_SYM", "_ZN4crdt8k_replayILi32ELj1EEEvNS_5PoolsEjjjPKj")  # (k_replay<32, SHAPE_REMOTE>)
 FILTER = int(os.environ.get("FILTER_CALL_LINE", "0"))
 FN = os.environ.get("FILTER_FN", "")
 DUMP = open(os.environ["DUMP_ADDR"], "w") if os.environ.get("DUMP_ADDR") else None  # per-instruction counts  # print this function's instructions (address, count/op)

@@ -217,6 +217,7 @@ struct crdt_engine {
   bool intern_on_device = false;  // crdt_stage_remote_replicated interns through k_intern
   int query_kernel = -1;  // crdt_set_query_kernel (-1: not set; CRDT_QUERY_PER_THREAD selects 1)
   bool published = false;
+  bool digested = false;   // k_digest ran on the current published index
   // A relayout (growth, crdt_fit) that failed after it began moving pools leaves some pools at
   // their new bases and the rest at the old ones: the engine is then unusable, and every call but
   // release / crdt_docs_alloc returns CRDT_E_NOMEM (no half-moved engine is replayed).
@@ -1082,7 +1083,23 @@ struct crdt_engine {
     }
     HIPCHK(hipEventRecord(ev[3], stream));
     published = true;
+    digested = false;
     materialized = false;
+    return 0;
+  }
+  // The per-document digests of the published state (k_digest, on request: the parity checker's
+  // summary, not part of the index publish builds for the queries)
+  int digest_now() {
+    if (!published) {
+      int r = publish();
+      if (r) return r;
+    }
+    if (digested || !n_docs) return 0;
+    u32 blocks = (u32)((n_docs + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    if (L == 32) hipLaunchKernelGGL(k_digest<32>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
+    else hipLaunchKernelGGL(k_digest<4>, dim3(blocks), dim3(256), 0, stream, pools_view(pools), pub_view(), (u32)n_docs);
+    HIPCHK(hipGetLastError());
+    digested = true;
     return 0;
   }
   int ensure_published() {
@@ -1753,10 +1770,8 @@ int crdt_digest_dev_async(crdt_engine* e, uint64_t* dev_out) {
   if (!valid(e) || !dev_out) return CRDT_E_ARG;
   int r = e->set_device();
   if (r) return r;
-  if (!e->published) {  // (the digests are publish's: never hand out the previous replay's)
-    r = e->publish();
-    if (r) return r;
-  }
+  r = e->digest_now();  // (the current state's: never the previous replay's)
+  if (r) return r;
   HIPCHK(hipMemcpyAsync(dev_out, e->digest, e->n_docs * 8, hipMemcpyDeviceToDevice, e->stream));
   return 0;
 }
@@ -1889,6 +1904,8 @@ int crdt_digest(crdt_engine* e, uint64_t* per_doc) {
   if (poisoned(e)) return CRDT_E_NOMEM;
   if (!valid(e) || !per_doc) return CRDT_E_ARG;
   int r = e->ensure_published();
+  if (r) return r;
+  r = e->digest_now();
   if (r) return r;
   HIPCHK(hipMemcpyAsync(per_doc, e->digest, e->n_docs * 8, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));

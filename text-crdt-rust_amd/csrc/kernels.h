@@ -285,6 +285,9 @@ __device__ __forceinline__ u64 wave_sum64(u64 v) {
 #define PUB_BIG_FEW_DOCS 1024u   // ... when the batch has at most this many documents
 #define PUB_BIG_MAX 16384u       // leaves from which it always does
 
+// A published document whose digest k_digest has not computed yet (publish writes it; k_digest
+// replaces it)
+constexpr u64 DIGEST_PENDING = 1ull;
 // Digest term of canonical span k (section 1; oracle/crdt_oracle.hpp digest()).
 __device__ __forceinline__ u64 span_hash(u32 k, const Span& sp) {
   return elem_hash(1, k, ((u64)sp.order << 32) | sp.ol, ((u64)sp.orr << 32) | (u32)sp.len);
@@ -306,21 +309,16 @@ struct RangeSum {
 // registers).  WRITE: spans go to canon/vpos from index `out` with visible offsets from `vis`;
 // skip_first: the range's first span continues the previous range's (not written); extra: the
 // signed length the range's last span continues by in later ranges.  !WRITE: fill `sum`.
-// HASH: add every written span's digest term (elem_hash section 1) to h, lane-partial (k_publish:
-// the spans are hashed from registers as they are written, not re-read).  Every written span's
-// first order also goes to corder.
-template <int L, bool WRITE, bool HASH = false>
+// Every written span's first order also goes to corder.
+template <int L, bool WRITE>
 __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg, u32 ng, u32 a, u32 b, Span* canon,
                                               u32* vpos, u32* corder, u32 ccap, u32& out, u32& vis, u32 skip_first,
-                                              i32 extra, RangeSum& sum, u64& h, uint4* ring = nullptr) {
+                                              i32 extra, RangeSum& sum) {
   const u32 l = lane_id();
   const Span* leaves = P.leaves + seg.leaf_base * L;
   const GroupRec* groups = P.groups + seg.grp_base;  // the root level, read in order from HBM
   const u32 vis0 = vis;
   u32 have = 0, skip = skip_first, nsp = 0, first_done = 0;
-  // HASH: spans are staged in this wave's 128-entry LDS ring as they are written and hashed 64 at a
-  // time (one digest evaluation per 64 spans instead of one per compaction step)
-  u32 hashed = out;
   Span open{0, 0, 0, 0};
   u32 open_vpos = 0;
   // the group holding leaf a: prefix of the groups' slot counts
@@ -415,7 +413,6 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
             else {
               if (l == 0u && out < ccap) {
                 canon[out] = open; vpos[out] = open_vpos; corder[out] = open.order;
-                if (HASH) ring[out & 127u] = make_uint4(open.order, open.ol, open.orr, (u32)open.len);
               }
               out++;
             }
@@ -432,7 +429,6 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
             canon[out + rank - sk] = sp;
             vpos[out + rank - sk] = vis + V - cl;
             corder[out + rank - sk] = v.x;
-            if (HASH) ring[(out + rank - sk) & 127u] = make_uint4(sp.order, sp.ol, sp.orr, (u32)sp.len);
           }
           out += firsts - sk;
           if (sk) skip = 0;
@@ -444,13 +440,6 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
       }
       sum.last = Span{rdlane(v.x, nn - 1u), rdlane(v.y, nn - 1u), rdlane(v.z, nn - 1u), (i32)rdlane(v.w, nn - 1u)};
       vis += leaf_vis;
-      if (HASH) {  // every full block of 64 written spans: hashed from the ring, one span per lane
-        while (out - hashed >= 64u && hashed + 64u <= ccap) {
-          uint4 x = ring[(hashed + l) & 127u];
-          h += span_hash(hashed + l, Span{x.x, x.y, x.z, (i32)x.w});
-          hashed += 64u;
-        }
-      }
     }
     idx = base;
   }
@@ -461,16 +450,8 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
       open.len += extra;
       if (l == 0 && out < ccap) {
         canon[out] = open; vpos[out] = open_vpos; corder[out] = open.order;
-        if (HASH) ring[out & 127u] = make_uint4(open.order, open.ol, open.orr, (u32)open.len);
       }
       out++;
-    }
-  }
-  if (HASH) {  // the rest of the ring (< 128 spans)
-    u32 end = out < ccap ? out : ccap;
-    for (; hashed < end; hashed += 64u) {
-      uint4 x = ring[(hashed + l) & 127u];
-      if (hashed + l < end) h += span_hash(hashed + l, Span{x.x, x.y, x.z, (i32)x.w});
     }
   }
   sum.spans = nsp;
@@ -484,10 +465,10 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
 // rank.  Per document 2 bits per order + 4 B per span are written instead of 4 B per item order.
 // Reads go through L2 (ld_l2): other lanes wrote them.  Wave `wv` of `nwv` takes every nwv-th
 // chunk; the word prefix is one contiguous word range per wave plus a cross-wave carry (lds_c:
-// nwv u32 of LDS, k_publish_big only).  Returns this wave's share of the canonical-span hash.
-template <int NWV, bool HASH = true>
-__device__ __forceinline__ u64 publish_index(const PubOut& O, const DocSeg& seg, const DocState& s, const Span* canon,
-                                             u32 out, u32 wv, u32* lds_c) {
+// nwv u32 of LDS, k_publish_big only).
+template <int NWV>
+__device__ __forceinline__ void publish_index(const PubOut& O, const DocSeg& seg, const DocState& s, const Span* canon,
+                                              u32 out, u32 wv, u32* lds_c) {
   const u32 l = lane_id();
 #ifdef PUB_NO_INDEX
   const u32 nw = pub_words(seg.ord_cap), used = 0u;
@@ -500,11 +481,9 @@ __device__ __forceinline__ u64 publish_index(const PubOut& O, const DocSeg& seg,
   for (u32 i = wv * 64u + l; i < used; i += 64u * NWV) bits[i] = 0u;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (NWV > 1) __syncthreads();
-  u64 h = 0;
   for (u32 k0 = wv * 64u; k0 < out; k0 += 64u * NWV) {
     u32 k = k0 + l;
     Span sp = k < out ? canon[k] : Span{0, 0, 0, 0};
-    if (HASH && k < out) h += span_hash(k, sp);
 #ifndef PUB_NO_INDEX
     // nearby spans share bitmap words: OR each distinct word's bits across the wave first, then
     // one atomic per word (same-address atomics serialise at L2)
@@ -571,7 +550,6 @@ __device__ __forceinline__ u64 publish_index(const PubOut& O, const DocSeg& seg,
     }
   }
 #endif
-  return h;
 }
 
 // The digest's other sections (client_with_order, deletes, double deletes, txns + parents,
@@ -622,7 +600,6 @@ __device__ __forceinline__ u64 digest_counts(const DocState& s, u32 out) {
 // 8,192 documents in 1.33 rounds)
 template <int L>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_publish(Pools P, PubOut O, u32 n, const u32* list, u32 xw) {
-  __shared__ uint4 s_ring[WAVES_PER_BLOCK][128];  // written spans awaiting the digest (compact_range)
   u32 d;
   if (!wave_doc(WAVES_PER_BLOCK, list, n, d)) return;
   WaveGPU<L> w;
@@ -637,28 +614,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
   u32* vpos = O.vpos + seg.canon_base;
   u32 out = 0, vis = 0;
   RangeSum sum{};
-  u64 h = 0;
-#ifdef PUB_NO_DIGEST  // (diagnostic: what the digest costs inside k_publish)
-  compact_range<L, true, false>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, O.corder + seg.canon_base, seg.canon_cap,
-                                out, vis, 0u, 0, sum, h, s_ring[threadIdx.x >> 6]);
-#else
-  compact_range<L, true, true>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, O.corder + seg.canon_base, seg.canon_cap,
-                               out, vis, 0u, 0, sum, h, s_ring[threadIdx.x >> 6]);
-#endif
+  compact_range<L, true>(P, seg, s.ng, 0u, s.n_leaves, canon, vpos, O.corder + seg.canon_base, seg.canon_cap,
+                         out, vis, 0u, 0, sum);
   if (out > seg.canon_cap) {  // canonical spans beyond the planned capacity: report, never write past it
     if (l == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
     return;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (pub_words(seg.ord_cap) > xw) h += publish_index<1, false>(O, seg, s, canon, out, 0u, nullptr);
-#ifndef PUB_NO_DIGEST
-  h += digest_tables<L>(P, seg, s, w);
-#endif
-  h = wave_sum64(h);
+  if (pub_words(seg.ord_cap) > xw) publish_index<1>(O, seg, s, canon, out, 0u, nullptr);
   if (l == 0) {
     O.canon_n[d] = out;
     O.len[d] = s.len;
-    O.digest[d] = mix64(h ^ digest_counts(s, out));
+    O.digest[d] = DIGEST_PENDING;  // (k_digest computes it on request)
   }
 }
 
@@ -669,7 +636,6 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
   __shared__ RangeSum s_sum[NWV];
   __shared__ u32 s_base[NWV], s_vbase[NWV], s_skip[NWV], s_c[NWV], s_total;
   __shared__ i32 s_extra[NWV];
-  __shared__ u64 s_h[NWV];
   const u32 d = list[blockIdx.x];
   const u32 l = lane_id(), wv = uni(threadIdx.x >> 6);
   WaveGPU<L> w;
@@ -685,9 +651,8 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
   const u32 a = (u32)((u64)s.n_leaves * wv / NWV), b = (u32)((u64)s.n_leaves * (wv + 1u) / NWV);
   u32 out = 0, vis = 0;
   RangeSum sum{};
-  u64 h0 = 0;
   u32* corder = O.corder + seg.canon_base;
-  compact_range<L, false>(P, seg, s.ng, a, b, canon, vpos, corder, seg.canon_cap, out, vis, 0u, 0, sum, h0);
+  compact_range<L, false>(P, seg, s.ng, a, b, canon, vpos, corder, seg.canon_cap, out, vis, 0u, 0, sum);
   if (l == 0) s_sum[wv] = sum;
   __syncthreads();
   if (wv == 0) {  // boundary resolution, lane = range
@@ -713,7 +678,7 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
   vis = s_vbase[wv];
   RangeSum sum2{};
   compact_range<L, true>(P, seg, s.ng, a, b, canon, vpos, corder, seg.canon_cap, out, vis, s_skip[wv], s_extra[wv],
-                         sum2, h0);
+                         sum2);
   const u32 total = s_total;
   if (total > seg.canon_cap) {
     if (threadIdx.x == 0) { O.canon_n[d] = 0; O.len[d] = s.len; O.digest[d] = 0; }
@@ -721,18 +686,35 @@ __global__ __launch_bounds__(64 * PUB_BIG_WAVES) void k_publish_big(Pools P, Pub
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
-  u64 h = publish_index<NWV>(O, seg, s, canon, total, wv, s_c);
-  if (wv == 0) h += digest_tables<L>(P, seg, s, w);
-  h = wave_sum64(h);
-  if (l == 0) s_h[wv] = h;
-  __syncthreads();
+  publish_index<NWV>(O, seg, s, canon, total, wv, s_c);
   if (threadIdx.x == 0) {
-    u64 t = 0;
-    for (u32 k = 0; k < NWV; k++) t += s_h[k];
     O.canon_n[d] = total;
     O.len[d] = s.len;
-    O.digest[d] = mix64(t ^ digest_counts(s, total));
+    O.digest[d] = DIGEST_PENDING;  // (k_digest computes it on request)
   }
+}
+
+// k_digest: the 64-bit state digest of every published document (oracle/crdt_oracle.hpp digest():
+// canonical spans, then the RLE tables and the counts), one wave per document, run on request
+// (crdt_digest, crdt_digest_dev_async) after a publish -- the digest is the parity checker's
+// summary of a state, not part of the flat index the queries read, so publish does not compute
+// it.  Documents publish refused (not OK, or past their planned index capacity) keep digest 0.
+template <int L>
+__global__ __launch_bounds__(256) void k_digest(Pools P, PubOut O, u32 n) {
+  u32 d;
+  if (!wave_doc(WAVES_PER_BLOCK, nullptr, n, d)) return;
+  if (O.digest[d] != DIGEST_PENDING) return;
+  WaveGPU<L> w;
+  DocState s = w.ldT(P.st + d);
+  DocSeg seg = w.ld_seg(P.seg + d);
+  const u32 l = lane_id();
+  const u32 out = O.canon_n[d];
+  const Span* canon = O.canon + seg.canon_base;
+  u64 h = 0;
+  for (u32 k = l; k < out; k += 64) h += span_hash(k, canon[k]);
+  h += digest_tables<L>(P, seg, s, w);
+  h = wave_sum64(h);
+  if (l == 0) O.digest[d] = mix64(h ^ digest_counts(s, out));
 }
 
 // ---------------------------------------------------------------------------------------------
