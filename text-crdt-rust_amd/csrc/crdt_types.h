@@ -141,6 +141,10 @@ inline u32 opq(u32 x) { return x; }
 CRDT_HD bool can_append(const Span& a, const Span& b) {  // span.rs:47-53
   return ((a.len > 0) == (b.len > 0)) && b.order == a.order + slen(a) && b.ol == b.order - 1 && b.orr == a.orr;
 }
+// ... branch-free, for per-lane operands (bitwise: && on lane values compiles to exec-masked branches)
+CRDT_HD bool can_append_b(const Span& a, const Span& b) {
+  return ((a.len > 0) == (b.len > 0)) & (b.order == a.order + slen(a)) & (b.ol == b.order - 1) & (b.orr == a.orr);
+}
 // The same test as early exits, for wave-uniform operands (the replay's scalar code): a branch per
 // condition instead of lane-mask booleans.  (can_append stays branch-free for lane-parallel use.)
 CRDT_HD bool can_append_u(const Span& a, const Span& b) {

@@ -346,10 +346,13 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
     // counts stores too, so an unpipelined load would wait behind them).
     constexpr u32 PER = 64u / (u32)L;
     u32 sub = l / (u32)L;
+    // (lane-parallel conditions below are bitwise, not short-circuit: && on per-lane values
+    // compiles to exec-masked branches; the load is unconditional from a valid leaf, then masked)
+    // (the masking happens when the step uses the entries, so a prefetched load is not waited for)
     auto ld = [&](u32 i) -> uint4 {
       u32 li = i + sub;
       u32 leaf = shfl(mydl, li < iend ? li : 0u);
-      return li < iend ? *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1))) : uint4{0, 0, 0, 0};
+      return *(const uint4*)(leaves + (u64)leaf * L + (l & (u32)(L - 1)));
     };
     // PUB_DEPTH steps of loads in flight (Little's law: one wave's 1 KiB per step is too little to
     // cover HBM latency at 8 waves per SIMD)
@@ -362,6 +365,10 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
 #endif
     for (u32 i = i0; i < iend; i += PER) {
       uint4 v = vn;
+      {  // lanes of leaves past the group's range: empty
+        bool in = i + sub < iend;
+        v = uint4{in ? v.x : 0u, in ? v.y : 0u, in ? v.z : 0u, in ? v.w : 0u};
+      }
 #if PUB_DEPTH >= 3
       vn = vn2;
       vn2 = vn3;
@@ -376,7 +383,8 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
       u32 nn = (u32)__popcll(VM);
       if (PER > 1) {
         u64 below = (1ull << l) - 1ull;
-        u32 dst = v.w != 0u ? (u32)__popcll(VM & below) : nn + (u32)__popcll(~VM & below);
+        u32 c1 = (u32)__popcll(VM & below);  // (valid entries below this lane; the empty ones are l - c1)
+        u32 dst = v.w != 0u ? c1 : nn + l - c1;
         int ad = (int)(dst << 2);
         v.x = (u32)__builtin_amdgcn_ds_permute(ad, (int)v.x);
         v.y = (u32)__builtin_amdgcn_ds_permute(ad, (int)v.y);
@@ -388,8 +396,8 @@ __device__ __forceinline__ void compact_range(const Pools& P, const DocSeg& seg,
       Span e{v.x, v.y, v.z, (i32)v.w};
       u32 px = shfl(v.x, l - 1u), py = shfl(v.y, l - 1u), pz = shfl(v.z, l - 1u), pw = shfl(v.w, l - 1u);
       Span prev = l == 0u ? sum.last : Span{px, py, pz, (i32)pw};
-      bool app = valid && (l != 0u || have) && can_append(prev, e);
-      bool start = valid && !app;
+      bool app = valid & ((l != 0u) | (have != 0u)) & can_append_b(prev, e);
+      bool start = valid & !app;
       u64 M = ballot(start);
       u32 len_u = valid ? v.w : 0u;
       u32 Pl = wave_incl_scan(len_u);  // signed lengths, two's complement sums
