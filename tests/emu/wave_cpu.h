@@ -113,6 +113,16 @@ struct WaveCPU {
     if (k >= 0) out = b[k];
     return k;
   }
+  template <class T> i32 search_run_recent(const T* b, u32 n, u32 x, T& out) const {
+    if (n <= 64u) return search_run(b, n, x, out);
+    WCPU_MEM(b + n - 64u, sizeof(T) * 64u, 0);
+    if (rkey(b[n - 64u]) > x) return search_run(b, n - 64u, x, out);
+    u32 k = n - 64u;
+    while (k + 1u < n && rkey(b[k + 1u]) <= x) k++;
+    if (x - rkey(b[k]) >= rlen(b[k])) return -1;
+    out = b[k];
+    return (i32)k;
+  }
   i32 search_cwo(const CwoRun* b, u32 n, u32 x) const { return search(b, n, x); }
   DDBlk ld_ddblk(const DDBlk* p) const { return *p; }
   void st_ddblk(DDBlk* p, const DDBlk& v) const { *p = v; }

@@ -954,7 +954,7 @@ struct Replayer {
       }
     }
     ARun r;
-    if (w.search_run(arun() + base, cnt, seq, r) < 0) return false;
+    if (w.search_run_recent(arun() + base, cnt, seq, r) < 0) return false;  // (recent runs first)
     order = r.order + (seq - r.key);
     return true;
   }

@@ -293,6 +293,20 @@ struct WaveGPU {
     __builtin_memcpy(&out, f, 16);
     return needle < f[0] + rlen(out) ? (i32)(lo + t) : -1;
   }
+  // As search_run, the last 64 runs first (one coalesced 1 KB load, no top level): a recent key --
+  // a round-start frontier head of a concurrent history, a few dozen runs back -- is answered there
+  template <class T>
+  __device__ __forceinline__ i32 search_run_recent(const T* base, u32 n, u32 needle, T& out) const {
+    if (n <= 64u) return search_run(base, n, needle, out);
+    u32 lo = n - 64u;
+    uint4 v = *(const uint4*)&base[lo + lane()];
+    u64 m = ballot(v.x <= needle);  // (keys ascend: a prefix of the lanes)
+    if (!(m & 1ull)) return search_run(base, lo, needle, out);
+    u32 t = 63 - __builtin_clzll(m);
+    u32 f[4] = {rdlane(v.x, t), rdlane(v.y, t), rdlane(v.z, t), rdlane(v.w, t)};
+    __builtin_memcpy(&out, f, 16);
+    return needle < f[0] + rlen(out) ? (i32)(lo + t) : -1;
+  }
   __device__ __forceinline__ static u32 rlen(const ARun& r) { return r.len; }
   __device__ __forceinline__ static u32 rlen(const CwoRun& r) { return r.len; }
   __device__ __forceinline__ static u32 rlen(const DDRun& r) { return r.len; }
