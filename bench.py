@@ -264,7 +264,8 @@ TRAFFIC_WORKLOAD = {"k_replay": "automerge-paper remote, one clean launch",
                     "k_replay:config4": "config 4: generated random edits (20,000 ops/doc), one clean launch",
                     "k_replay:config3": "config 3: mixed local corpus, shared record streams, one clean launch",
                     "k_replay:config3_noshare": "config 3: mixed local corpus, per-document record streams, one clean launch",
-                    "k_replay:config5": "config 5: concurrent histories (1 M-char base, 16 agents), one clean launch"}
+                    "k_replay:config5": "config 5: concurrent histories (1 M-char base, 16 agents), one clean launch",
+                    "k_replay:config5d": "config 5: per-document concurrent histories (1 M-char base, 16 agents), one clean launch"}
 
 
 def measured_traffic(n_docs: int, kernel: str = "k_replay", workload: str = None):

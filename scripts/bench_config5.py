@@ -151,6 +151,9 @@ if not a.no_cpu:
 
 t = min(ts)
 rk = float(np.mean(rms))
+# the PMC pass this line's traffic comes from: per-document histories (scripts/gpu_pmc.sh c5d) or
+# the shared-history shape (c5)
+tw = "config5d" if (a.gen == "c" and a.distinct == a.docs and not a.share) else "config5"
 alg = int(32 * int(canon.sum()) + 24 * total_ops)
 print(json.dumps({
     "metric": "CRDT ops remapped+merged/sec (config 5: concurrent deletion-heavy remote merges)",
@@ -168,8 +171,8 @@ print(json.dumps({
                         "canonical_spans": sizes0["canon"], "len": sizes0["len"]}},
     "roofline": {"bound": "hbm", "achieved": alg / (rk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": alg / (rk * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                 "traffic": measured_traffic(a.docs, "k_replay", "config5") if a.leaf == 32 else None,
-                 "traffic_file": "profiles/traffic_k_replay_config5.json", "kernel": f"k_replay<{a.leaf}>",
+                 "traffic": measured_traffic(a.docs, "k_replay", tw) if a.leaf == 32 else None,
+                 "traffic_file": f"profiles/traffic_k_replay_{tw}.json", "kernel": f"k_replay<{a.leaf}>",
                  "kernel_ms": rk, "alg_bytes_per_launch": alg,
                  "alg_bytes_formula": "SURVEY 8(d): docs x (32 B x canonical spans + 24 B x ops)"},
     "kernels_ms": {"k_replay": rk, "k_publish": float(np.mean(pms))},

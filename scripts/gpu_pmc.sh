@@ -23,6 +23,7 @@ from bench import splitmix64; from crdt_amd.traces import load_trace
 n = [load_trace(x).n_patches for x in ('automerge-paper', 'rustcode', 'sveltecomponent')]
 print(round(sum(n[splitmix64(d) % 3] for d in range($D)) / $D))"); P="python scripts/prof_replay.py --docs $D --config3 --no-share --clean"; T="_config3_noshare"; LBL="config 3: mixed local corpus, per-document record streams, one clean launch";;
     c4) D=125000; OPS=20000; P="python scripts/prof_replay.py --docs $D --random 20000 --clean"; T="_config4"; LBL="config 4: generated random edits (20,000 ops/doc), one clean launch";;
+    c5d) D=8192; OPS=65537; P="python scripts/bench_config5.py --docs 8192 --steps 1 --no-cpu --check-docs 2"; T="_config5d"; LBL="config 5: per-document concurrent histories (1 M-char base, 16 agents), one clean launch";;
     c5) D=8192; OPS=65537; P="python scripts/prof_replay.py --docs $D --config5 --clean"; T="_config5"; LBL="config 5: concurrent histories (1 M-char base, 16 agents), one clean launch";;
   esac
   TAG=_$w P="$P" bash scripts/gpu_pmc_all.sh > gpurun_out/pmc_$w.log 2>&1 || { cat gpurun_out/pmc_$w.log; exit 1; }

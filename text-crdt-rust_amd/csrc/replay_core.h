@@ -1472,10 +1472,17 @@ struct Replayer {
           if (!get_item(c, other_order)) break;
           if (other_order == item.orr) break;
           Span oe = w.cget(c.idx);  // get_item ensured c.leaf
-          Cursor olc;
-          CRDT_STAT(40, 1); CRDT_STAT(41 + olc_stat(origin_left_at_offset(oe, c.off), left), 1);
-          if (!cursor_after(origin_left_at_offset(oe, c.off), false, olc)) return ST_UNKNOWN_ID;
-          int r = cmp(olc, left);
+          u32 oo = origin_left_at_offset(oe, c.off);
+          CRDT_STAT(40, 1); CRDT_STAT(41 + olc_stat(oo, left), 1);
+          // the other item's origin_left is the new item's own (a concurrent sibling): the same
+          // cursor (cursor_after of one order, found above), so cmp is 0 without looking it up --
+          // no order -> leaf lookup and no peek at left's leaf once the scan has left it
+          int r = 0;
+          if (oo != item.ol) {
+            Cursor olc;
+            if (!cursor_after(oo, false, olc)) return ST_UNKNOWN_ID;
+            r = cmp(olc, left);
+          }
           if (r < 0) break;
           if (r == 0) {
             u32 oa;
