@@ -61,6 +61,7 @@ else:
     wires = config5_wires([0xC5000000 + s for s in range(a.distinct)], base_len=a.base, n_agents=a.agents, rounds=a.rounds,
                           ops=a.ops, threads=threads)
 gen_s = time.time() - t0
+print(f"generated {a.distinct} histories in {gen_s:.1f} s", file=sys.stderr, flush=True)
 ops_of = [wire_ops(w)[0] for w in wires]
 doc_w = [d % a.distinct for d in range(a.docs)]
 total_ops = sum(ops_of[k] for k in doc_w)
@@ -71,6 +72,7 @@ e.share_streams(a.share)
 t0 = time.time()
 e.apply_remote_wire(list(range(a.docs)), [wires[k] for k in doc_w], stage_only=True)
 stage_s = time.time() - t0
+print(f"staged {a.docs} documents in {stage_s:.1f} s", file=sys.stderr, flush=True)
 st = e.run()  # untimed: capacity growth, index sizing
 assert (st == 0).all(), np.unique(st)
 e.publish_async()

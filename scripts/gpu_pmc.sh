@@ -26,7 +26,8 @@ print(round(sum(n[splitmix64(d) % 3] for d in range($D)) / $D))"); P="python scr
     c5d) D=8192; OPS=65537; P="python scripts/bench_config5.py --docs 8192 --steps 1 --no-cpu --check-docs 2"; T="_config5d"; LBL="config 5: per-document concurrent histories (1 M-char base, 16 agents), one clean launch";;
     c5) D=8192; OPS=65537; P="python scripts/prof_replay.py --docs $D --config5 --clean"; T="_config5"; LBL="config 5: concurrent histories (1 M-char base, 16 agents), one clean launch";;
   esac
-  TAG=_$w P="$P" bash scripts/gpu_pmc_all.sh > gpurun_out/pmc_$w.log 2>&1 || { cat gpurun_out/pmc_$w.log; exit 1; }
+  PT=150; [ $w = c5d ] && PT=400  # (c5d: generation + staging of 8,192 histories in every pass)
+  TAG=_$w P="$P" PT=$PT bash scripts/gpu_pmc_all.sh > gpurun_out/pmc_$w.log 2>&1 || { cat gpurun_out/pmc_$w.log; exit 1; }
   python scripts/traffic_from_pmc.py $D profiles/traffic_k_replay$T.json k_replay _$w "$LBL" || exit 1
   python scripts/sq_summary.py profiles/${RN}_sq_k_replay_${w}_${D}_${V}.json $D $OPS _$w "$LBL" > /dev/null || exit 1
   cp profiles/traffic_k_replay$T.json profiles/${RN}_traffic_k_replay_${w}_${D}_${V}.json
