@@ -91,6 +91,7 @@ for k, t in enumerate(traces):
     cpu_s += s
 t = min(ts)
 print(json.dumps({
+    "build_id": crdt_amd.build_id(),
     "metric": "CRDT ops remapped+merged/sec (config 3: mixed local corpus)", "value": ops / t, "unit": "ops/s",
     "n_gpus": 1, "steps": a.steps, "ms_per_step": t * 1e3, "higher_is_better": True, "dtype": "u32",
     "data": "synthetic-from-trace: benchmark_data traces, doc d replays trace splitmix64(d) % 3",

@@ -158,6 +158,7 @@ rk = float(np.mean(rms))
 tw = "config5d" if (a.gen == "c" and a.distinct == a.docs and not a.share) else "config5"
 alg = int(32 * int(canon.sum()) + 24 * total_ops)
 print(json.dumps({
+    "build_id": crdt_amd.build_id(),
     "metric": "CRDT ops remapped+merged/sec (config 5: concurrent deletion-heavy remote merges)",
     "value": total_ops / t, "unit": "ops/s", "n_gpus": 1, "steps": a.steps, "ms_per_step": t * 1e3,
     "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",

@@ -78,6 +78,7 @@ for docs in (1, a.docs):
                  "parity_ok": bool((dg == np.uint64(o.digest())).all()), "hbm_bytes": e.mem_bytes()}
     e.close()
 print(json.dumps({
+    "build_id": crdt_amd.build_id(),
     "metric": "kevin: 5M front inserts (benches/yjs.rs:51-62)", "unit": "ops/s", "ops_per_doc": n,
     "single_doc": res[1], "batch": res[a.docs],
     "cpu_single_thread": {"seconds": cpu_s, "ops_per_s": n / cpu_s, "kind": "port",

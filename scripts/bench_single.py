@@ -102,6 +102,7 @@ for wl in a.workloads.split(","):
     ok = bool(int(e.digests()[0]) == int(odg))
     e.close()
     print(json.dumps({
+        "build_id": crdt_amd.build_id(),
         "metric": f"single-document replay time ({wl})", "value": ms, "unit": "ms", "n_gpus": 1, "steps": a.reps,
         "higher_is_better": False, "dtype": "u32", "data": "reference trace" if wl != "kevin" else "synthetic (the bench's shape)",
         "config": {"workload": desc, "docs": 1, "ops": ops, "leaf_cap": 32},
