@@ -319,6 +319,36 @@ def test_config5_full_size():
                 check_queries_sampled(e, 0, o)
 
 
+def test_config5_per_document_histories():
+    # config 5's measured shape (scripts/bench_config5.py default): every document replays its own
+    # seeded history (tests/gen/config5_gen.cpp: its own ops and delivery order) from its own record
+    # copy, 96 documents in one launch at a reduced size; every digest against the oracle's replay
+    # of that document's history, both layouts
+    from fuzz_gen import config5_wires
+    wires = config5_wires([0xC5100000 + s for s in range(96)], base_len=1 << 15, n_agents=16, rounds=8, ops=16,
+                          threads=8)
+    assert len({w for w in wires}) == len(wires)  # (distinct histories)
+    odg = []
+    for w in wires:
+        o = OracleDoc(32, 16)
+        assert o.apply_remote_wire(w) == 0
+        odg.append(o.digest())
+    for L in (32, 4):
+        e = crdt_amd.Engine(len(wires), L)
+        e.share_streams(False)
+        st = e.apply_remote_wire(list(range(len(wires))), wires)
+        assert (st == 0).all(), st
+        dg = e.digests()
+        if L == 32:
+            assert [int(x) for x in dg] == odg
+        else:
+            for i in (0, 47, 95):
+                o = OracleDoc(4, 8)
+                assert o.apply_remote_wire(wires[i]) == 0
+                assert int(dg[i]) == o.digest(), i
+        e.close()
+
+
 @pytest.mark.parametrize("L", [32, 4])
 def test_config1_every_op_probed(L):
     # BASELINE config 1 ("checking every position <-> CRDT-location lookup"): after EVERY txn of
