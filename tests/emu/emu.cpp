@@ -341,6 +341,23 @@ int emu_run_wire(void* h, const uint8_t* wire, size_t len, uint32_t leaf_div) {
   return d->run();
 }
 
+// A remote wire, then local txns by agent `name` (interned after the wire's agents, as a document
+// that merged the wire and then edited locally names it), in one stream of the general shape.
+int emu_run_wire_local(void* h, const uint8_t* wire, size_t len, const char* name, uint32_t ntxn, const uint32_t* counts,
+                       const uint32_t* patches3, uint32_t leaf_div) {
+  EmuDoc* d = (EmuDoc*)h;
+  WireView wv;
+  if (!wv.parse(wire, len)) return ST_BAD_INPUT;
+  StreamNeeds nd;
+  d->recs.clear();
+  encode_remote(d->recs, nd, d->agents, wv);
+  u16 agent = (u16)d->agents.get_or_create(name);
+  const uint32_t* p = patches3;
+  for (uint32_t t = 0; t < ntxn; t++) { encode_local_txn(d->recs, nd, agent, p, counts[t]); p += 3 * counts[t]; }
+  d->prepare(nd, true, leaf_div);
+  return d->run();
+}
+
 // sizes: [n_raw, n_leaves, n_cwo, n_del, n_dd, n_txn, n_parents, n_frontier, n_agents, next_order, len, rec_pos]
 void emu_sizes(void* h, uint64_t* s) {
   EmuDoc* d = (EmuDoc*)h;

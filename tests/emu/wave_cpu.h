@@ -376,6 +376,41 @@ struct WaveCPU {
     if (m) f[m] = last;
     return m + 1u;
   }
+  void fr_lanes_load(const u32* f, u32 n) {
+    WCPU_MEM(f, 4ull * n, 0);
+    for (u32 k = 1; k < n; k++) x[FR_S0 + k - 1u] = f[k];
+  }
+  void fr_lanes_store(u32* f, u32 n) const {
+    WCPU_MEM(f, 4ull * n, 1);
+    for (u32 k = 1; k < n; k++) f[k] = x[FR_S0 + k - 1u];
+  }
+  u32 frontier_advance_x(u32 nfr, u32 f0, const u32* pp, u32 np, u32 p0, u32 first, u32 last, u32 cap, u32& nf0,
+                         u32* f) {
+    WCPU_MEM(pp, 4ull * np, 0);
+    std::vector<u32> h(nfr);
+    for (u32 k = 0; k < nfr; k++) h[k] = k == 0 ? f0 : x[FR_S0 + k - 1u];
+    for (u32 k = 0; k < nfr; k++) if (h[k] == first) return 0u;
+    auto has = [&](u32 v) {
+      if (np == 0) return false;
+      if (p0 == v) return true;
+      for (u32 j = 1; j < np; j++) if (pp[j] == v) return true;
+      return false;
+    };
+    std::vector<u32> kept;
+    for (u32 k = 0; k < nfr; k++) if (!has(h[k])) kept.push_back(h[k]);
+    u32 m = (u32)kept.size();
+    if (m + 1u > cap) return INVALID;
+    nf0 = m ? kept[0] : last;
+    if (m <= FR_LANES) {
+      for (u32 k = 1; k < m; k++) x[FR_S0 + k - 1u] = kept[k];
+      if (m) x[FR_S0 + m - 1u] = last;
+    } else {
+      WCPU_MEM(f, 4ull * (m + 1u), 1);
+      for (u32 k = 1; k < m; k++) f[k] = kept[k];
+      f[m] = last;
+    }
+    return m + 1u;
+  }
   u32 front_scan(u32 b0, u32 nv, u32 agent, u32 len) const {
     u32 n = 1;
     for (u32 j = b0 + 1; j < nv; j++) {

@@ -38,6 +38,7 @@ def lib():
         L.emu_agent.argtypes = [vp, C.c_char_p]
         L.emu_run_local.argtypes = [vp, u16, u32, P(u32), P(u32), u32]
         L.emu_run_wire.argtypes = [vp, C.c_char_p, C.c_size_t, u32]
+        L.emu_run_wire_local.argtypes = [vp, C.c_char_p, C.c_size_t, C.c_char_p, u32, P(u32), P(u32), u32]
         L.emu_run_random.argtypes = [vp, u16, u32, u32, u32]
         L.emu_run_local_probed.argtypes = [vp, u16, u32, P(u32), P(u32), P(u32), P(u32), u32]
         L.emu_sizes.argtypes = [vp, P(C.c_uint64)]
@@ -75,6 +76,11 @@ class EmuDoc:
         ans = np.zeros((c.shape[0], 4), np.uint32)
         st = self.L.emu_run_local_probed(self.h, agent, c.shape[0], _p(c), _p(p), _p(q), _p(ans), leaf_div)
         return st, ans
+
+    def run_wire_local(self, wire: bytes, name: str, counts, patches, leaf_div: int = 48) -> int:
+        c = np.ascontiguousarray(counts, np.uint32)
+        p = np.ascontiguousarray(patches, np.uint32)
+        return self.L.emu_run_wire_local(self.h, wire, len(wire), name.encode(), c.shape[0], _p(c), _p(p), leaf_div)
 
     def run_wire(self, wire: bytes, leaf_div: int = 48) -> int:
         return self.L.emu_run_wire(self.h, wire, len(wire), leaf_div)

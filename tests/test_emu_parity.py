@@ -240,3 +240,37 @@ def test_local_txn_parts(L):
         if so == 0:
             assert e.check() == ""
             assert diff_states(o.export(), e.export()) == []
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_wide_frontier(seed):
+    # frontiers past the context lanes (replay_core.h FR_S0: heads 1..24 in lanes, more in HBM):
+    # 40 concurrent agents grow the frontier to 41 heads and the round-start merges shrink it back,
+    # so the heads cross between lanes and HBM both ways; local txns after the wire take the whole
+    # frontier as their parents (heads -> parent pool); tight caps add capacity stops and resumes
+    from fuzz_gen import config5_wire
+    w = config5_wire(seed, base_len=4000, n_agents=40, rounds=5, ops=3)
+    c = np.array([1, 1], np.uint32)
+    pt = np.array([[5, 0, 3], [0, 2, 0]], np.uint32)
+    for L in (32, 4):
+        o = OracleDoc(L, 16 if L == 32 else 8)
+        assert o.apply_remote_wire(w) == 0
+        assert len(o.export()["frontier"]) > 25
+        e = EmuDoc(L)
+        assert e.run_wire(w, 48) == 0
+        assert e.check() == ""
+        assert diff_states(o.export(), e.export()) == []
+        assert o.apply_trace(o.agent("local-editor"), c, pt) == 0
+        e = EmuDoc(L)
+        assert e.run_wire_local(w, "local-editor", c, pt, 48) == 0
+        assert e.check() == ""
+        assert diff_states(o.export(), e.export()) == []
+    # frontiers that stay within the lanes, then a local txn (config 5's 16 agents)
+    w = config5_wire(seed, base_len=4000, n_agents=16, rounds=5, ops=3)
+    o = OracleDoc()
+    assert o.apply_remote_wire(w) == 0
+    assert 2 <= len(o.export()["frontier"]) <= 25
+    assert o.apply_trace(o.agent("local-editor"), c, pt) == 0
+    e = EmuDoc(32)
+    assert e.run_wire_local(w, "local-editor", c, pt, 48) == 0
+    assert diff_states(o.export(), e.export()) == []

@@ -349,6 +349,38 @@ def test_config5_per_document_histories():
         e.close()
 
 
+def test_wide_frontier_then_local():
+    # frontier heads live in context lanes up to 25 heads (replay_core.h FR_S0), in HBM past that:
+    # documents with 40 concurrent agents (frontiers to 41 heads, crossing both ways) and with 16
+    # (always in the lanes), replayed as remote wires, then a second launch of local txns by a new
+    # agent on every document (begin() reloads the heads; the local txn takes them as parents);
+    # every digest and the first documents' whole state against the oracle, both layouts
+    from fuzz_gen import config5_wire
+    wires = [config5_wire(300 + s, base_len=4000, n_agents=40 if s % 2 else 16, rounds=5, ops=3) for s in range(8)]
+    txs = [[5, 0, 3], [0, 2, 0]]
+    for L in (32, 4):
+        e = crdt_amd.Engine(len(wires), L)
+        st = e.apply_remote_wire(list(range(len(wires))), wires)
+        assert (st == 0).all(), st
+        ids = e.agent_intern(list(range(len(wires))), ["local-editor"] * len(wires))
+        st = e.apply_local([(d, [(int(ids[d]), [t]) for t in txs]) for d in range(len(wires))])
+        assert (st == 0).all(), st
+        dg = e.digests()
+        for d, w in enumerate(wires):
+            o = OracleDoc(L, 16 if L == 32 else 8)
+            assert o.apply_remote_wire(w) == 0
+            if d % 2:
+                assert len(o.export()["frontier"]) > 25
+            a = o.agent("local-editor")
+            assert a == int(ids[d])
+            for t in txs:
+                assert o.apply_local(a, [t]) == 0
+            assert int(dg[d]) == o.digest(), (L, d)
+            if d < 2:
+                assert_same(e.export(d), o.export())
+        e.close()
+
+
 @pytest.mark.parametrize("L", [32, 4])
 def test_config1_every_op_probed(L):
     # BASELINE config 1 ("checking every position <-> CRDT-location lookup"): after EVERY txn of

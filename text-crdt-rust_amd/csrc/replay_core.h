@@ -77,6 +77,11 @@ enum : u32 {
   // next_order == F_BASE: fast commits only advance next_order (and the author's item_orders
   // tail, which the fast path reads); materialize_tails() brings them up to date.
   F_BASE,
+  // Frontier heads 1..n_fr-1 while n_fr <= FR_LANES + 1 (head 0 is T_FR0): slot FR_S0 + k - 1 holds
+  // head k.  A concurrent history's frontier (one head per active agent) is then advanced in the
+  // context register, with no dependent HBM load per remote txn; the HBM array is written back
+  // with the tails (flush_tails) and holds larger frontiers.
+  FR_S0 = 104,
   // x2: leaf cache bookkeeping
   C_LEAF = 128, C_N, C_VIS, C_NOW, C_BLK, C_I, C_VSTART, C_DIRTY, C_VS_OK /* (unused) */,
   C_SUCC, C_SUCC_ORD,  // successor leaf of the cached one (INVALID: not known) + its first order (INVALID: not known)
@@ -100,7 +105,8 @@ enum : u32 {
 };
 static_assert(P_LAG + 1 < 64, "read-only slots live in the first context register");
 static_assert(S_PROF3 - S_BASE + 1 == sizeof(DocState) / 4, "DocState slot mirror");
-static_assert(F_BASE < 128, "DocState and the flags live in the second context register");
+static_assert(F_BASE < FR_S0, "DocState and the flags live in the second context register, below the frontier heads");
+constexpr u32 FR_LANES = 128u - FR_S0;  // frontier heads kept in context lanes
 static_assert(N_SLOTS <= 192, "three context registers");
 
 template <class W, int L>
@@ -282,6 +288,8 @@ struct Replayer {
       p(T_TX_ORDER, t.order); p(T_TX_LEN, t.len); p(T_TX_SHADOW, t.shadow);
     }
     p(T_FR0, w.ld(fr()));
+    n = g(S_N_FR);
+    if (n <= FR_LANES + 1u) w.fr_lanes_load(fr(), n);
     n = g(S_N_DDB);
     if (n <= 64u * DDT_LDS) w.ddt_rebuild(ddb(), 0u, n);
   }
@@ -307,6 +315,8 @@ struct Replayer {
     if (n) w.st(&w.at(txns(), n - 1)->len, g(T_TX_LEN));
     flush_agent();
     w.st(fr(), g(T_FR0));
+    n = g(S_N_FR);
+    if (n <= FR_LANES + 1u) w.fr_lanes_store(fr(), n);
   }
   CRDT_HD void flush_agent() {
     u32 a = g(T_AG_ID), cnt = g(T_AG_CNT);
@@ -1174,17 +1184,23 @@ struct Replayer {
       if (nfr == 1) {
         if (f0 == first) return ST_FRONTIER;
         if (par_contains(pp, np, p0, f0)) p(T_FR0, last);
-        else { w.st(f + 1, last); p(S_N_FR, 2); }
+        else { p(FR_S0, last); p(S_N_FR, 2); }  // (head 1 in its context lane)
       } else if (nfr <= 64u && np <= 64u) {
         // lane-parallel (one head / one parent per lane): heads that name `first` make the txn a
-        // duplicate; heads among the parents go, the rest stay in order, `last` joins
-        u32 nf0;
-        u32 r = w.frontier_advance(f, nfr, f0, pp, np, p0, first, last, g(K_FR), nf0);
+        // duplicate; heads among the parents go, the rest stay in order, `last` joins.  Heads in
+        // context lanes (FR_S0) while they fit, else in HBM; a frontier that crosses the bound
+        // moves with the result
+        u32 nf0, r;
+        bool lanes = nfr <= FR_LANES + 1u;
+        if (lanes) r = w.frontier_advance_x(nfr, f0, pp, np, p0, first, last, g(K_FR), nf0, f);
+        else r = w.frontier_advance(f, nfr, f0, pp, np, p0, first, last, g(K_FR), nf0);
         if (r == 0u) return ST_FRONTIER;
         if (r == INVALID) return ST_CAPACITY;  // (fits() reserved room for nfr + 1 heads)
+        if (!lanes && r <= FR_LANES + 1u) w.fr_lanes_load(f, r);
         p(S_N_FR, r);
         p(T_FR0, nf0);
       } else {
+        if (nfr <= FR_LANES + 1u) w.fr_lanes_store(f, nfr);  // (this form reads and writes the heads in HBM)
         for (u32 k = 0; k < nfr; k++) if ((k == 0 ? f0 : w.ld(f + k)) == first) return ST_FRONTIER;
         u32 m = 0, nf0 = f0;
         for (u32 k = 0; k < nfr; k++) {
@@ -1198,13 +1214,15 @@ struct Replayer {
         if (m + 1 > g(K_FR)) return ST_CAPACITY;  // (fits() reserved room for nfr + 1 heads)
         if (m == 0) nf0 = last;
         else w.st(f + m, last);
+        if (m + 1u <= FR_LANES + 1u) w.fr_lanes_load(f, m + 1u);
         p(S_N_FR, m + 1);
         p(T_FR0, nf0);
       }
     } else {
       np = nfr;
       p0 = f0;
-      for (u32 k = 1; k < np; k++) w.st(pp + k, w.ld(f + k));
+      if (np <= FR_LANES + 1u) w.fr_lanes_store(pp, np);  // (the heads become the txn's parents)
+      else for (u32 k = 1; k < np; k++) w.st(pp + k, w.ld(f + k));
       p(T_FR0, last);
       p(S_N_FR, 1);
     }

@@ -879,6 +879,48 @@ struct WaveGPU {
     if (m) f[m] = last;  // (every lane stores the same value)
     return m + 1u;
   }
+  // ---- frontier heads 1..n-1 in context lanes (replay_core.h FR_S0: x1 lane FR_S0 - 64 + k - 1
+  // holds head k, n <= FR_LANES + 1), moved in from / out to the HBM array f[1..n)
+  static constexpr u32 FR_L0 = FR_S0 - 64u;
+  __device__ __forceinline__ void fr_lanes_load(const u32* f, u32 n) {
+    u32 l = lane();
+    bool mine = (l >= FR_L0) & (l < FR_L0 + n - 1u);
+    u32 v = f[mine ? l - FR_L0 + 1u : 0u];  // (clamped address: unconditional load)
+    x1 = mine ? v : x1;
+  }
+  __device__ __forceinline__ void fr_lanes_store(u32* f, u32 n) const {
+    u32 l = lane();
+    if ((l >= FR_L0) & (l < FR_L0 + n - 1u)) f[l - FR_L0 + 1u] = x1;
+  }
+  // frontier_advance with heads 1.. read from the context lanes; the new heads go back to the
+  // lanes (a push: kept head of rank a >= 1 to lane FR_L0 + a - 1, `last` after them) while they
+  // fit, else to f[1..] in HBM
+  __device__ __forceinline__ u32 frontier_advance_x(u32 nfr, u32 f0, const u32* pp, u32 np, u32 p0, u32 first,
+                                                    u32 last, u32 cap, u32& nf0, u32* f) {
+    u32 l = lane();
+    bool in = l < nfr;
+    u32 fv = shfl(x1, l + FR_L0 - 1u);  // (lane l >= 1: head l; lane 0's is replaced)
+    fv = l == 0u ? f0 : fv;
+    if (ballot(in && fv == first)) return 0u;
+    u32 pv = np > 1u ? pp[l < np ? l : 0u] : 0u;  // (parent 0 is p0: pp[0] is not written yet)
+    pv = l == 0u ? p0 : pv;
+    bool hit = false;
+    for (u32 j = 0; j < np; j++) hit |= fv == rdlane(pv, j);
+    u64 keep = ballot(in && !hit);
+    u32 m = (u32)__popcll(keep);
+    if (m + 1u > cap) return INVALID;
+    nf0 = m ? rdlane(fv, (u32)__builtin_ctzll(keep)) : last;
+    u32 at = (u32)__popcll(keep & ((1ull << l) - 1ull));
+    bool mv = ((keep >> l) & 1ull) && at >= 1u;
+    if (m <= FR_LANES) {
+      u32 moved = (u32)__builtin_amdgcn_ds_permute((int)((mv ? FR_L0 + at - 1u : 0u) << 2), (int)fv);
+      if (m) x1 = (l >= FR_L0) & (l < FR_L0 + m - 1u) ? moved : l == FR_L0 + m - 1u ? last : x1;
+    } else {
+      if (mv) f[at] = fv;
+      f[m] = last;
+    }
+    return m + 1u;
+  }
   // runs {key0 + j, t0 - j, 1} for j < cnt (backspaced deletes), lane-parallel
   __device__ __forceinline__ void st_del_run(DelRun* p, u32 cnt, u32 key0, u32 t0) const {
     for (u32 j = lane(); j < cnt; j += 64) {
