@@ -1,3 +1,5 @@
+# Round-6 shape instances: GPU tests, then the same-box A/B of CRDT_NO_SHAPES=1 (every stream in the
+# general instance) against the shape instances (scripts/gpu_ab_env.sh) -> profiles/r06_ab_shapes.txt.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

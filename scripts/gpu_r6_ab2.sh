@@ -1,3 +1,5 @@
+# Local-only shape instance: GPU tests, then the same-box A/B against the previous build
+# (scripts/gpu_ab_libs.sh) -> profiles/r06_ab_local_shape.txt.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out

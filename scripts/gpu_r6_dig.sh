@@ -1,3 +1,5 @@
+# Publish timing at one build over the A/B workloads (scripts/gpu_ab_libs.sh with one library):
+# profiles/r06_digest_on_request.txt and r06_publish_branchfree.txt were made this way.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
