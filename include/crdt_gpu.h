@@ -182,9 +182,7 @@ int crdt_last_materialize_ms(crdt_engine* e, double* ms);
 /* ListCRDT::len (doc.rs:484-486) */
 int crdt_doc_len(crdt_engine* e, uint64_t n, const uint32_t* doc, uint32_t* len);
 int crdt_doc_status(crdt_engine* e, int32_t* status /* n_docs */);
-/* 64-bit digest of each document's canonical state (DESIGN.md "Digest"; same as the oracle).
- * Computed on request (k_digest) for the documents published since the last digest: the publish
- * itself builds only the flat index the queries read. */
+/* 64-bit digest of each document's canonical state (DESIGN.md "Digest"; same as the oracle). */
 int crdt_digest(crdt_engine* e, uint64_t* per_doc /* n_docs */);
 /* Canonical spans of each document's published index (YjsSpan::can_append runs; sizes[2] of
  * crdt_export_sizes for every document at once: the roofline's per-document span counts). */
@@ -215,8 +213,8 @@ int crdt_fit_note(crdt_engine* e, int apply);
 // /root/reference/src/list/doc.rs:544-569).  Device-side, async on the engine stream; the next
 // reset + crdt_run_async replays the new documents.
 int crdt_reseed_random_async(crdt_engine* e, uint64_t seed, uint64_t id_base);
-// crdt_digest into a device buffer (n_docs u64), async on the engine stream after a publish
-// (crdt_publish_async): computes the pending digests (k_digest), then copies them.
+// crdt_digest into a device buffer (n_docs u64), async on the engine stream after the publish
+// that computes the digests (crdt_publish_async).
 int crdt_digest_dev_async(crdt_engine* e, uint64_t* dev_out);
 // on != 0: documents staged in one call from the same host stream (crdt_stage_local_shared,
 // crdt_stage_remote_replicated) read one device copy of it instead of a copy each (records
