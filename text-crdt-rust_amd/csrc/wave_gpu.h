@@ -914,7 +914,7 @@ struct WaveGPU {
     bool mv = ((keep >> l) & 1ull) && at >= 1u;
     if (m <= FR_LANES) {
       u32 moved = (u32)__builtin_amdgcn_ds_permute((int)((mv ? FR_L0 + at - 1u : 0u) << 2), (int)fv);
-      if (m) x1 = (l >= FR_L0) & (l < FR_L0 + m - 1u) ? moved : l == FR_L0 + m - 1u ? last : x1;
+      if (m) x1 = ((l >= FR_L0) & (l < FR_L0 + m - 1u)) ? moved : l == FR_L0 + m - 1u ? last : x1;
     } else {
       if (mv) f[at] = fv;
       f[m] = last;
